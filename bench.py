@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Headline benchmark: forward + backward gate applications per second of a differentiable
+state-vector circuit on MI355X (BASELINE.json metric), with the HBM roofline of the dominant
+kernel and the CPU baseline (the C/OpenMP restatement of the reference kernels) beside it.
+
+Workload (SURVEY.md §8d, config C2's generator at the metric's target size): n = 28 qubits, f32,
+L = 20 layers of [Haar 1-qubit variable gate on every qubit; Haar 2-qubit variable gates on
+(i+1, i) for even i, then odd i], DiffQ1Density on every qubit, loss sum_q Re tr(rho_q sigma_z).
+One step = Circuit.forward (all densities to the host) + Circuit.backward (all gate gradients
+to the host), i.e. one loss-and-gradient call as in example_vqse_ising.py:107-133.
+
+value = gates x steps / wall time (every gate is applied once forward and once in the fused
+reverse sweep); inputs are resident in HBM before the timed region (gate matrices are 16-256 B
+host arrays passed per call, as in the reference API).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): each rank runs the workload on
+its own GPU as an independent replica ("replicas": the sharded-state path is future work, see
+DESIGN.md), value = sum over ranks, time = max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "differentiable-quantum-circuit-cuda_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--qubits", type=int, default=28)
+    ap.add_argument("--layers", type=int, default=20)
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--seed", type=int, default=24)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-layers", type=int, default=1,
+                    help="layers of the CPU baseline sample (full n)")
+    ap.add_argument("--cpu-qubits", type=int, default=None)
+    ap.add_argument("--pmc", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    ap.add_argument("--micro", action="store_true", help="per-kernel bandwidth sweep")
+    return ap.parse_args()
+
+
+def build_circuit(q, n, layers, seed, precision):
+    from oracle import oracle as O  # workload generator only (gate matrices, instruction list)
+    ins, var = O.layered_circuit(n, layers, seed)
+    c = q.circuit_class(precision)(n)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    dt = c.dtype
+    vg = [np.ascontiguousarray(g, dtype=dt) for g in var]
+    return c, ins, vg
+
+
+def sigma_z_cotangents(ndens, dt):
+    # d/d rho of Re tr(rho sigma_z) is sigma_z^T; the qdc wiring conjugates it (circuit.py:193)
+    return [np.ascontiguousarray(np.diag([1.0, -1.0]).astype(dt)) for _ in range(ndens)]
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def select_device(local):
+    # HIP device selection for the native library (it uses the current device)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    err = hip.hipSetDevice(ctypes.c_int(local))
+    if err != 0:
+        raise RuntimeError(f"hipSetDevice({local}) failed: {err}")
+
+
+def cpu_baseline(args, n, layers):
+    """Time the oracle's C/OpenMP restatement of the reference algorithm (unfused uncompute /
+    grad / pull-back and allocate-conj-gate-add density injection, circuit.rs:266-429) on a
+    bounded sample of the same workload."""
+    from oracle import oracle as O
+    from oracle.cref import CRefOps
+    ops = CRefOps(args.precision)
+    ins, var = O.layered_circuit(n, layers, args.seed)
+    dt = ops.state_dtype
+    o = O.OracleCircuit(n, dt, ops=ops)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    t0 = time.perf_counter()
+    dens = o.forward([], var)
+    o.backward(sigma_z_cotangents(len(dens), dt), [], var)
+    dt_s = time.perf_counter() - t0
+    gates = sum(1 for k, _ in ins if k < 10)
+    return {"value": gates / dt_s, "unit": "gate-applications/s (fwd+bwd)",
+            "cores": ops.threads(), "kind": "port",
+            "sample": f"{layers} layer(s) of the same circuit at n={n} {args.precision}: "
+                      f"{gates} gates fwd+bwd + {len(dens)} densities in {dt_s:.1f} s "
+                      f"(oracle/cpu_ref.c, OpenMP)"}
+
+
+def micro(args):
+    """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse."""
+    import quantum_differentiable_circuit as q
+    n, prec = args.qubits, args.precision
+    dt = np.complex64 if prec == "f32" else np.complex128
+    rng = np.random.default_rng(0)
+    rows = []
+
+    def run(label, setup):
+        c = q.circuit_class(prec)(n)
+        var = setup(c)
+        c.forward([], var)  # warm-up
+        c.backward(sigma_z_cotangents(1, dt), [], var)
+        c.profile(True)
+        for _ in range(3):
+            c.forward([], var)
+            c.backward(sigma_z_cotangents(1, dt), [], var)
+        stats = c.profile_collect()
+        c.profile(False)
+        for k, s in stats.items():
+            if s["total_ms"] > 0 and k not in ("finalize",):
+                gbs = s["algo_bytes"] / (s["total_ms"] * 1e-3) / 1e9
+                rows.append((label, k, s["launches"], s["total_ms"] / s["launches"], gbs))
+                print(f"{label:14s} {k:18s} n={s['launches']:4d} {s['total_ms'] / s['launches']:8.3f} ms"
+                      f" {gbs:8.1f} GB/s  {gbs / HBM_PEAK_GBS:6.1%}", flush=True)
+        del c
+
+    reps = 8
+    for pos in range(n):
+        def s1(c, pos=pos):
+            for _ in range(reps):
+                c.add_q1_var_gate(pos)
+            c.get_q1_dens_op_with_grad(pos)
+            return [np.ascontiguousarray(O_haar(rng, 2), dtype=dt) for _ in range(reps)]
+        run(f"q1 {pos}", s1)
+    for pos2, pos1 in [(0, 1), (1, 0), (5, 20), (26, 27), (27, 0), (1, 2), (3, 9), (14, 13)]:
+        if max(pos2, pos1) >= n:
+            continue
+
+        def s2(c, pos2=pos2, pos1=pos1):
+            for _ in range(reps):
+                c.add_q2_var_gate(pos2, pos1)
+            for _ in range(reps):
+                c.add_q2_var_gate_diag(pos2, pos1)
+            c.get_q1_dens_op_with_grad(pos1)
+            return ([np.ascontiguousarray(O_haar(rng, 4), dtype=dt) for _ in range(reps)]
+                    + [np.exp(1j * rng.standard_normal(4)).astype(dt) for _ in range(reps)])
+        run(f"q2 {pos2},{pos1}", s2)
+    return rows
+
+
+def O_haar(rng, k):
+    from oracle import oracle as O
+    return O.haar_unitary(rng, k)
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    select_device(local)
+    import quantum_differentiable_circuit as q
+    if args.micro:
+        micro(args)
+        return
+
+    n = args.qubits
+    c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision)
+    ngates = len(vg)
+    cots = sigma_z_cotangents(sum(1 for k, _ in ins if k in (12, 13)), c.dtype)
+
+    for _ in range(args.warmup):
+        c.forward([], vg)
+        c.backward(cots, [], vg)
+    c.synchronize()
+
+    c.profile(True)
+    barrier(world)
+    c.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dens = c.forward([], vg)
+        grads = c.backward(cots, [], vg)
+    c.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier(world)
+    stats = c.profile_collect()
+    c.profile(False)
+
+    elapsed = max_over_ranks(elapsed, world)
+    total_gates = sum_over_ranks(float(ngates * args.steps), world)
+    value = total_gates / elapsed
+
+    # dominant kernel = the one with the largest share of measured device time
+    dom_name, dom = max(((k, v) for k, v in stats.items()), key=lambda kv: kv[1]["total_ms"])
+    avg_ms = dom["total_ms"] / dom["launches"]
+    bytes_per_launch = dom["algo_bytes"] / dom["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = Path(args.pmc) if args.pmc else ROOT / "profiles" / "pmc_traffic.json"
+    if pmc_path.exists():
+        try:
+            traffic = json.loads(pmc_path.read_text()).get(dom_name)
+        except Exception:  # noqa: BLE001
+            traffic = None
+    kernels = {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4),
+                   "GB/s": round(v["algo_bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)
+                   if v["total_ms"] > 0 else None,
+                   "share": round(v["total_ms"] / sum(s["total_ms"] for s in stats.values()), 4)}
+               for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"])}
+
+    # sanity: the loss gradient is finite and the densities are traces of 1
+    assert all(np.isfinite(g).all() for g in grads)
+    assert all(abs(np.trace(d) - 1) < 1e-3 for d in dens)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.cpu_qubits or n, args.cpu_layers)
+
+    if rank == 0:
+        state_gib = (1 << n) * (8 if args.precision == "f32" else 16) / 2**30
+        line = {
+            "metric": "gate-applications/sec (fwd+bwd) at n qubits",
+            "value": round(value, 3),
+            "unit": "gate-applications/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "c64 (f32)" if args.precision == "f32" else "c128 (f64)",
+            "data": "synthetic (seeded Haar-random gates, |0..0> initial state)",
+            "config": {"workload": f"C2 layered random circuit (configs[1] generator) at the "
+                                   f"metric's n={n}, fwd+bwd, 1 GPU per replica",
+                       "qubits": n, "layers": args.layers, "gates_per_step": ngates,
+                       "densities_per_step": len(cots), "state_GiB": state_gib,
+                       "parallelism": "replicas" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algo_bytes_per_launch": bytes_per_launch,
+                         "avg_launch_ms": round(avg_ms, 4)},
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,544 @@
+// qdc_device.hpp — host-side launch layer: per-stream context, partial-sum arena,
+// launch geometry, per-kernel event profiling, host small-matrix algebra.
+//
+// Replaces the reference's per-call host plumbing (src/primitives.cu:114-138 cuBLAS
+// handle per inverse, :255-292 malloc/launch/D2H/host-sum/free per reduction) with one
+// context per stream that owns every scratch buffer for its lifetime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "qdc/primitives.h"
+#include "qdc_kernels.hpp"
+
+namespace qdc {
+
+static_assert(sizeof(cx) == sizeof(qdc_complex), "complex layout");
+
+// ---------------------------------------------------------------------------------------
+// Errors: NULL = ok, else a message in thread-local storage (the caller never frees it;
+// the reference leaks a malloc'd string instead, primitives.cu:37-47).
+// ---------------------------------------------------------------------------------------
+inline const char* fail(const char* fmt, ...) {
+  static thread_local char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return buf;
+}
+
+#define QDC_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t qdc_e_ = (call);                                                        \
+    if (qdc_e_ != hipSuccess)                                                          \
+      return ::qdc::fail("HIP ERROR: call of a function \"%s\" in line %d of file %s " \
+                         "failed with %s.",                                            \
+                         #call, __LINE__, __FILE__, hipGetErrorName(qdc_e_));          \
+  } while (0)
+
+#define QDC_TRY(expr)                  \
+  do {                                 \
+    const char* qdc_m_ = (expr);       \
+    if (qdc_m_ != nullptr) return qdc_m_; \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Profiling: optional start/stop events around every launch of a context's stream.
+// Used by bench.py to measure each kernel's average duration inside the timed region.
+// ---------------------------------------------------------------------------------------
+struct ProfRecord {
+  const char* name;
+  double bytes;
+  hipEvent_t a, b;
+};
+
+struct Prof {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  std::vector<ProfRecord> recs;
+
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  void reset() {
+    used = 0;
+    recs.clear();
+  }
+  ~Prof() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Context: one HIP stream + the scratch it needs.  Every op of a context is ordered on its
+// stream; host-visible results synchronise that stream only.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NBMAX = 4096;  // max blocks of a reduction launch = partials per slot
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t grid_cap = 1u << 20;  // streaming launches: ~one item per thread (measured best)
+  uint32_t red_cap = 2048;   // target blocks of reduction launches (<= NBMAX)
+  // reduction arena
+  cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
+  cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
+  cx* host_results = nullptr;  // pinned [FIN_MAX][RED]
+  std::vector<uint32_t> pending_dst;
+  std::vector<uint32_t> pending_nb;
+  cx* pending_base = nullptr;
+  int pending_accumulate = 0;
+  Prof prof;
+
+  const char* init(int dev) {
+    device = dev;
+    QDC_HIP(hipSetDevice(dev));
+    QDC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    QDC_HIP(hipMalloc(&partials, sizeof(cx) * (size_t)FIN_MAX * NBMAX * RED));
+    QDC_HIP(hipMalloc(&results, sizeof(cx) * (size_t)FIN_MAX * RED));
+    QDC_HIP(hipHostMalloc(&host_results, sizeof(cx) * (size_t)FIN_MAX * RED));
+    if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
+    if (grid_cap < 1) grid_cap = 1;
+    if (red_cap < 1) red_cap = 1;
+    if (red_cap > NBMAX) red_cap = NBMAX;
+    return nullptr;
+  }
+  void destroy() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (partials) (void)hipFree(partials);
+    if (results) (void)hipFree(results);
+    if (host_results) (void)hipHostFree(host_results);
+    if (stream) (void)hipStreamDestroy(stream);
+    partials = results = host_results = nullptr;
+    stream = nullptr;
+  }
+
+
+  template <typename K, typename... Args>
+  const char* launch(const char* name, double bytes, K kernel, uint32_t grid, Args... args) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (prof.on) {
+      a = prof.get();
+      b = prof.get();
+      if (a) (void)hipEventRecord(a, stream);
+    }
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(BLOCK), 0, stream, args...);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return fail("HIP ERROR: launch of kernel %s failed with %s.", name, hipGetErrorName(e));
+    if (prof.on && a && b) {
+      (void)hipEventRecord(b, stream);
+      prof.recs.push_back({name, bytes, a, b});
+    }
+    return nullptr;
+  }
+
+  // --- reduction slots -----------------------------------------------------------------
+  // A reduction kernel writes its per-block partials into the next free slot; the slot is
+  // later summed into base[dst*RED .. +RED) by k_finalize.  All pending slots share one base.
+  const char* begin_reduction(cx* base, int accumulate) {
+    if (base != pending_base || accumulate != pending_accumulate) QDC_TRY(flush());
+    pending_base = base;
+    pending_accumulate = accumulate;
+    if (pending_dst.size() == (size_t)FIN_MAX) QDC_TRY(flush());
+    return nullptr;
+  }
+  cx* slot_ptr() const { return partials + pending_dst.size() * (size_t)NBMAX * RED; }
+  void commit(uint32_t dst, uint32_t nb) {
+    pending_dst.push_back(dst);
+    pending_nb.push_back(nb);
+  }
+  const char* flush() {
+    size_t i = 0;
+    while (i < pending_dst.size()) {
+      // group consecutive slots with equal partial counts into one launch
+      size_t j = i;
+      fin_table tab{};
+      while (j < pending_dst.size() && pending_nb[j] == pending_nb[i]) {
+        tab.dst[j - i] = pending_dst[j];
+        ++j;
+      }
+      QDC_TRY(launch("finalize", 0.0, k_finalize,
+                     (uint32_t)(j - i), (const cx*)(partials + i * (size_t)NBMAX * RED),
+                     (uint64_t)NBMAX * RED, pending_nb[i], tab, pending_base,
+                     pending_accumulate));
+      i = j;
+    }
+    pending_dst.clear();
+    pending_nb.clear();
+    return nullptr;
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Launch geometry (SURVEY.md §2.1 index rules, in 16-byte-chunk space)
+// ---------------------------------------------------------------------------------------
+struct Plan {
+  bool tile = false;  // TILE family (a target at chunk bit 0..5) or DIRECT family
+  int R = 2;
+  int mode = 0;       // DIRECT row layout (see rows<R, MODE>)
+  geo g{};
+  tgeo tg{};
+};
+
+inline uint64_t nchunks_of(uint32_t n) { return ((uint64_t)1 << n) / VEC; }
+inline uint32_t log2u(uint64_t x) {
+  uint32_t r = 0;
+  while ((x >> r) > 1) ++r;
+  return r;
+}
+// a target whose pair mate sits in another lane of the same wave
+inline bool is_low(uint32_t q) { return q >= (uint32_t)LV && (q - LV) < (uint32_t)LOWBITS; }
+
+// items per thread for block-contiguous iteration: keep the grid near `target` blocks
+inline uint32_t per_thread(uint64_t items, uint32_t target) {
+  uint64_t it = 1;
+  while ((uint64_t)BLOCK * it * target < items) it <<= 1;
+  return (uint32_t)it;
+}
+
+// q1: R = 2, pos2 == pos1 == target.  q2: R = 4.
+inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_states,
+                      uint32_t grid_target) {
+  Plan p;
+  p.R = R;
+  const uint64_t nch = nchunks_of(n);
+  const bool low = is_low(pos1) || (R == 4 && is_low(pos2));
+  if (!low) {
+    if (R == 2) {
+      if ((int)pos1 < LV) {
+        p.mode = 1;
+        p.g.items = nch;
+      } else {
+        p.mode = 0;
+        p.g.lo = pos1 - LV;
+        p.g.sa = (uint64_t)1 << p.g.lo;
+        p.g.items = nch / 2;
+      }
+    } else {
+      const uint32_t lo = pos2 < pos1 ? pos2 : pos1;
+      const uint32_t hi = pos2 < pos1 ? pos1 : pos2;
+      if ((int)lo < LV) {
+        p.mode = (lo == pos1) ? 1 : 2;
+        p.g.hi = hi - LV;
+        p.g.sa = (uint64_t)1 << p.g.hi;
+        p.g.items = nch / 2;
+      } else {
+        p.mode = 0;
+        p.g.lo = lo - LV;
+        p.g.hi = hi - LV;
+        p.g.sa = (uint64_t)1 << (pos2 - LV);
+        p.g.sb = (uint64_t)1 << (pos1 - LV);
+        p.g.items = nch / 4;
+      }
+    }
+    p.g.it = per_thread(p.g.items, grid_target);
+    return p;
+  }
+  // TILE: 256*K chunks per state per tile, K = 4 (one state) or 2 (two states)
+  p.tile = true;
+  const uint32_t T = two_states ? 9 : 10;
+  const uint32_t cbits = log2u(nch);
+  const uint32_t teff = cbits < T ? cbits : T;
+  uint32_t l = teff, h = 0, hb0 = 0;
+  if (R == 4) {
+    // the non-low target may lie beyond the tile's contiguous bits: make it a row bit
+    const uint32_t far = is_low(pos1) ? pos2 : pos1;
+    if (far >= (uint32_t)LV && far - LV >= teff) {
+      h = 1;
+      l = teff - 1;
+      hb0 = far - LV;
+    }
+  }
+  auto local_bit = [&](uint32_t q) -> uint32_t {
+    if (q < (uint32_t)LV || q - LV < l) return q;
+    return LV + l;  // row bit 0
+  };
+  p.tg.l = l;
+  p.tg.h = h;
+  p.tg.hb0 = hb0;
+  p.tg.hb1 = 0;
+  p.tg.t1 = local_bit(pos1);
+  p.tg.t2 = local_bit(pos2);
+  p.tg.ntiles = nch >> (l + h);
+  uint64_t tpb = 1;
+  while (tpb * grid_target < p.tg.ntiles) tpb <<= 1;
+  p.tg.tpb = (uint32_t)tpb;
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host small-matrix algebra (gates are 2x2 / 4x4, row-major).
+// ---------------------------------------------------------------------------------------
+template <int R>
+inline mat<R> to_mat(const qdc_complex* h) {
+  mat<R> m;
+  for (int i = 0; i < R * R; ++i) m.a[i] = {h[i].re, h[i].im};
+  return m;
+}
+template <int R>
+inline mat<R> transpose(const mat<R>& m) {
+  mat<R> t;
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < R; ++j) t.a[i * R + j] = m.a[j * R + i];
+  return t;
+}
+template <int R>
+inline mat<R> conj_transpose(const mat<R>& m) {
+  mat<R> t;
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < R; ++j) t.a[i * R + j] = {m.a[j * R + i].x, -m.a[j * R + i].y};
+  return t;
+}
+inline diag4 to_diag(const qdc_complex* h) {
+  diag4 d;
+  for (int i = 0; i < 4; ++i) d.a[i] = {h[i].re, h[i].im};
+  return d;
+}
+inline diag4 conj_diag(const diag4& d) {
+  diag4 c;
+  for (int i = 0; i < 4; ++i) c.a[i] = {d.a[i].x, -d.a[i].y};
+  return c;
+}
+
+// Inverse of a row-major R x R matrix, restating cublas{C,Z}matinvBatched as the reference
+// calls it (primitives.cu:114-138): cuBLAS is column-major, so it factorises A^T by LU with
+// partial pivoting; info = i (1-based) when U(i,i) is exactly zero → "U(i, i) is zero.".
+// Computed in long double, rounded once to the working precision.
+template <int R>
+inline const char* inverse(const mat<R>& a, mat<R>& out) {
+  using C = std::complex<long double>;
+  C m[R][R], inv[R][R];
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < R; ++j) {
+      // column-major view of the row-major buffer: M = A^T
+      m[i][j] = C(a.a[j * R + i].x, a.a[j * R + i].y);
+      inv[i][j] = (i == j) ? C(1, 0) : C(0, 0);
+    }
+  for (int k = 0; k < R; ++k) {
+    int piv = k;
+    long double best = std::abs(m[k][k]);
+    for (int r = k + 1; r < R; ++r) {
+      long double v = std::abs(m[r][k]);
+      if (v > best) {
+        best = v;
+        piv = r;
+      }
+    }
+    if (best == 0.0L) return fail("U(%d, %d) is zero.", k + 1, k + 1);
+    if (piv != k)
+      for (int j = 0; j < R; ++j) {
+        std::swap(m[k][j], m[piv][j]);
+        std::swap(inv[k][j], inv[piv][j]);
+      }
+    const C d = m[k][k];
+    for (int j = 0; j < R; ++j) {
+      m[k][j] /= d;
+      inv[k][j] /= d;
+    }
+    for (int r = 0; r < R; ++r) {
+      if (r == k) continue;
+      const C f = m[r][k];
+      if (f == C(0, 0)) continue;
+      for (int j = 0; j < R; ++j) {
+        m[r][j] -= f * m[k][j];
+        inv[r][j] -= f * inv[k][j];
+      }
+    }
+  }
+  // inv = (A^T)^-1 = (A^-1)^T; its column-major storage is A^-1 row-major.
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < R; ++j)
+      out.a[i * R + j] = {(real)inv[j][i].real(), (real)inv[j][i].imag()};
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------------------
+// Op launchers (all asynchronous on ctx.stream)
+// ---------------------------------------------------------------------------------------
+inline double state_bytes(uint32_t n) { return (double)((uint64_t)1 << n) * sizeof(cx); }
+
+inline uint32_t blocks_of(const Plan& p) {
+  if (p.tile) return (uint32_t)((p.tg.ntiles + p.tg.tpb - 1) / p.tg.tpb);
+  return (uint32_t)((p.g.items + (uint64_t)BLOCK * p.g.it - 1) / ((uint64_t)BLOCK * p.g.it));
+}
+
+// Launch one gate-shaped op (any OP, R) on the family the plan selected.
+template <int OP, int R>
+inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, const mat<R>& A,
+                          const mat<R>& B, const Plan& p, cx* partials) {
+  chunk* fc = reinterpret_cast<chunk*>(f);
+  chunk* bc = reinterpret_cast<chunk*>(b);
+  const uint32_t grid = blocks_of(p);
+  if (p.tile) {
+    constexpr int K = op_two_states(OP) ? 2 : 4;
+    return c.launch(name, bytes, k_tile<OP, R, K>, grid, fc, bc, A, B, p.tg, partials);
+  }
+  if (p.mode == 0)
+    return c.launch(name, bytes, k_direct<OP, R, 0, (R == 2 ? 2 : 1)>, grid, fc, bc, A, B, p.g,
+                    partials);
+  if (p.mode == 1)
+    return c.launch(name, bytes, k_direct<OP, R, 1, (R == 2 ? 4 : 2)>, grid, fc, bc, A, B, p.g,
+                    partials);
+  if constexpr (R == 4)
+    return c.launch(name, bytes, k_direct<OP, 4, 2, 2>, grid, fc, bc, A, B, p.g, partials);
+  return fail("invalid plan");
+}
+
+template <int R>
+inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
+                     bool reduces) {
+  return plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap);
+}
+
+template <int R>
+inline const char* apply_dense(Ctx& c, cx* s, const mat<R>& m, uint32_t pos2, uint32_t pos1,
+                               uint32_t n, const char* name) {
+  const Plan p = plan_for<R>(c, n, pos2, pos1, false, false);
+  return run_op<OP_APPLY, R>(c, name, 2.0 * state_bytes(n), s, nullptr, m, m, p, nullptr);
+}
+
+inline dgeo diag_geo(uint32_t n, uint32_t pos2, uint32_t pos1, uint32_t target) {
+  dgeo g;
+  g.nchunks = nchunks_of(n);
+  g.it = per_thread(g.nchunks, target);
+  g.p2 = pos2;
+  g.p1 = pos1;
+  return g;
+}
+inline uint32_t diag_blocks(const dgeo& g) {
+  return (uint32_t)((g.nchunks + (uint64_t)BLOCK * g.it - 1) / ((uint64_t)BLOCK * g.it));
+}
+
+inline const char* apply_diag(Ctx& c, cx* s, const diag4& d, uint32_t pos2, uint32_t pos1,
+                              uint32_t n, const char* name) {
+  const dgeo g = diag_geo(n, pos2, pos1, c.grid_cap);
+  return c.launch(name, 2.0 * state_bytes(n), k_diag<DIAG_APPLY, 4>, diag_blocks(g),
+                  reinterpret_cast<chunk*>(s), (chunk*)nullptr, d, d, g, (cx*)nullptr);
+}
+
+// reduction slot helper: run `launch(partials)` producing `nb` partials for base[dst]
+template <class F>
+inline const char* reduce_into(Ctx& c, cx* base, uint32_t dst, int accumulate, uint32_t nb,
+                               F&& launch) {
+  if (nb > NBMAX) return fail("reduction grid %u exceeds %u", nb, NBMAX);
+  QDC_TRY(c.begin_reduction(base, accumulate));
+  QDC_TRY(launch(c.slot_ptr()));
+  c.commit(dst, nb);
+  return nullptr;
+}
+
+// density of one (R = 2) or two (R = 4) qubits → reduction slot for base[dst]
+template <int R>
+inline const char* density(Ctx& c, const cx* s, uint32_t pos2, uint32_t pos1, uint32_t n,
+                           cx* base, uint32_t dst, int accumulate) {
+  const Plan p = plan_for<R>(c, n, pos2, pos1, false, true);
+  const mat<R> z{};
+  return reduce_into(c, base, dst, accumulate, blocks_of(p), [&](cx* out) {
+    return run_op<OP_DENSITY, R>(c, R == 2 ? "density_q1" : "density_q2", state_bytes(n),
+                                 const_cast<cx*>(s), nullptr, z, z, p, out);
+  });
+}
+
+template <int R>
+inline const char* grad_dense(Ctx& c, const cx* f, const cx* b, uint32_t pos2, uint32_t pos1,
+                              uint32_t n, cx* base, uint32_t dst, int accumulate) {
+  const Plan p = plan_for<R>(c, n, pos2, pos1, true, true);
+  const mat<R> z{};
+  return reduce_into(c, base, dst, accumulate, blocks_of(p), [&](cx* out) {
+    return run_op<OP_GRAD, R>(c, R == 2 ? "grad_q1" : "grad_q2", 2.0 * state_bytes(n),
+                              const_cast<cx*>(f), const_cast<cx*>(b), z, z, p, out);
+  });
+}
+
+inline const char* grad_diag(Ctx& c, const cx* f, const cx* b, uint32_t pos2, uint32_t pos1,
+                             uint32_t n, cx* base, uint32_t dst, int accumulate) {
+  const dgeo g = diag_geo(n, pos2, pos1, c.red_cap);
+  const diag4 z{};
+  return reduce_into(c, base, dst, accumulate, diag_blocks(g), [&](cx* out) {
+    return c.launch("grad_q2_diag", 2.0 * state_bytes(n), k_diag<DIAG_GRAD, 4>, diag_blocks(g),
+                    const_cast<chunk*>(reinterpret_cast<const chunk*>(f)),
+                    const_cast<chunk*>(reinterpret_cast<const chunk*>(b)), z, z, g, out);
+  });
+}
+
+// Fused reverse step for a dense gate.  grad_base == nullptr → constant gate (no gradient).
+template <int R>
+inline const char* reverse_dense(Ctx& c, cx* f, cx* b, const mat<R>& A, const mat<R>& B,
+                                 uint32_t pos2, uint32_t pos1, uint32_t n, cx* grad_base,
+                                 uint32_t dst) {
+  const double bytes = 4.0 * state_bytes(n);
+  const char* name = (R == 2) ? "reverse_q1" : "reverse_q2";
+  if (grad_base) {
+    const Plan p = plan_for<R>(c, n, pos2, pos1, true, true);
+    return reduce_into(c, grad_base, dst, 0, blocks_of(p), [&](cx* out) {
+      return run_op<OP_REVERSE_GRAD, R>(c, name, bytes, f, b, A, B, p, out);
+    });
+  }
+  const Plan p = plan_for<R>(c, n, pos2, pos1, true, false);
+  return run_op<OP_REVERSE, R>(c, name, bytes, f, b, A, B, p, nullptr);
+}
+
+inline const char* reverse_diag(Ctx& c, cx* f, cx* b, const diag4& d, uint32_t pos2,
+                                uint32_t pos1, uint32_t n, cx* grad_base, uint32_t dst) {
+  chunk* fc = reinterpret_cast<chunk*>(f);
+  chunk* bc = reinterpret_cast<chunk*>(b);
+  const diag4 dc = conj_diag(d);
+  const double bytes = 4.0 * state_bytes(n);
+  if (grad_base) {
+    const dgeo g = diag_geo(n, pos2, pos1, c.red_cap);
+    return reduce_into(c, grad_base, dst, 0, diag_blocks(g), [&](cx* out) {
+      return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE_GRAD, 2>, diag_blocks(g), fc,
+                      bc, dc, d, g, out);
+    });
+  }
+  const dgeo g = diag_geo(n, pos2, pos1, c.grid_cap);
+  return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE, 2>, diag_blocks(g), fc, bc, dc,
+                  d, g, (cx*)nullptr);
+}
+
+template <int R>
+inline const char* inject(Ctx& c, const cx* f, cx* b, const mat<R>& m, uint32_t pos2,
+                          uint32_t pos1, uint32_t n, bool first) {
+  const Plan p = plan_for<R>(c, n, pos2, pos1, true, false);
+  const double bytes = (first ? 2.0 : 3.0) * state_bytes(n);
+  const char* name = (R == 2) ? "inject_q1" : "inject_q2";
+  if (first)
+    return run_op<OP_INJECT_FIRST, R>(c, name, bytes, const_cast<cx*>(f), b, m, m, p, nullptr);
+  return run_op<OP_INJECT, R>(c, name, bytes, const_cast<cx*>(f), b, m, m, p, nullptr);
+}
+
+// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>
+template <int OP>
+inline const char* elementwise(Ctx& c, const cx* src, cx* dst, uint32_t n) {
+  const uint64_t amps = (uint64_t)1 << n;
+  const uint64_t nch = amps / VEC > 0 ? amps / VEC : 1;
+  const uint32_t it = per_thread(nch, c.grid_cap);
+  const uint32_t grid = (uint32_t)((nch + (uint64_t)BLOCK * it - 1) / ((uint64_t)BLOCK * it));
+  const double bytes = (OP == 2 ? 3.0 : OP == 3 ? 1.0 : 2.0) * state_bytes(n);
+  static const char* names[4] = {"copy", "conj_and_double", "add", "set_standard"};
+  return c.launch(names[OP], bytes, k_elementwise<OP>, grid, src, dst, amps, it);
+}
+
+inline const char* set_standard(Ctx& c, cx* s, uint32_t n) {
+  return elementwise<3>(c, nullptr, s, n);
+}
+
+}  // namespace qdc

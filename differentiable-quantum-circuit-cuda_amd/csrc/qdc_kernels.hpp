@@ -1,0 +1,582 @@
+// qdc_kernels.hpp — hand-written CDNA4 (gfx950) kernels for the state-vector hot path.
+//
+// What the reference computes (src/primitives.cu, index rules in SURVEY.md §2.1) and how it
+// is laid out here:
+//
+//   * A state is 2^n interleaved complex amplitudes in HBM, moved in 16-byte "chunks"
+//     (global_load/store_dwordx4, nontemporal): VEC = 2 amplitudes per chunk in f32, 1 in f64.
+//   * Every kernel keeps each wave instruction on one contiguous KiB (64 lanes x 16 B).  Two
+//     kernel families guarantee that:
+//       - DIRECT kernels, when every target qubit is either inside the chunk (f32 qubit 0) or
+//         at chunk-index bit >= 6: a k-qubit gate reads its 2^k "rows" (the reference's
+//         INSERT_ZERO bit insertion, primitives.cu:104-105, in chunk space) as 2^k separate
+//         contiguous streams;
+//       - TILE kernels, when some target sits at chunk bit 0..5 (its pair mate lives in
+//         another lane of the same wave): a workgroup stages a tile of 256*K contiguous
+//         chunks (plus up to two "row" bits for a far target) through LDS, applies the gate
+//         on LDS, and writes the tile back.
+//   * Blocks own contiguous ranges of work (block-contiguous iteration, U items in flight):
+//     measured on MI355X this beats persistent grid-stride loops by 10-20 % (tools/bw_probe).
+//   * Reductions (densities, gate gradients) accumulate per thread, reduce the wave with
+//     64-lane butterflies and the block through LDS, and write one 16-complex partial per
+//     block; a finalize kernel sums partials in a fixed order (deterministic, no atomics, no
+//     host round trip per gate).
+//   * The reverse sweep is fused: one pass reads fwd and bwd once, uncomputes fwd,
+//     accumulates the gradient from (bwd, uncomputed fwd) and pulls bwd back — 4S bytes
+//     instead of the reference's 6S with a host sync in the middle (circuit.rs:320-326).
+//
+// Gate matrices travel as kernel arguments (kernarg → SGPRs), never as global __constant__
+// symbols, so there is no cross-thread race (README.md:13).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qdc {
+
+#ifdef QDC_F64
+using real = double;
+typedef double vec16 __attribute__((ext_vector_type(2)));
+#else
+using real = float;
+typedef float vec16 __attribute__((ext_vector_type(4)));
+#endif
+
+struct cx {
+  real x, y;
+};
+
+constexpr int VEC = 16 / (int)sizeof(cx);  // amplitudes per 16-byte chunk: 2 (f32) / 1 (f64)
+constexpr int LV = (VEC == 2) ? 1 : 0;      // log2(VEC)
+constexpr int BLOCK = 256;                  // 4 waves of 64
+constexpr int RED = 16;                     // complex values per reduction partial
+constexpr int LOWBITS = 6;                  // chunk bits that index lanes of one wave
+
+struct alignas(16) chunk {
+  cx v[VEC];
+};
+
+template <int R>
+struct mat {
+  cx a[R * R];  // row-major
+};
+struct diag4 {
+  cx a[4];
+};
+
+// nontemporal 16-byte chunk access (streams larger than every cache level)
+__device__ __forceinline__ chunk ldc(const chunk* p) {
+  const vec16 v = __builtin_nontemporal_load(reinterpret_cast<const vec16*>(p));
+  return __builtin_bit_cast(chunk, v);
+}
+__device__ __forceinline__ void stc(chunk* p, const chunk& c) {
+  __builtin_nontemporal_store(__builtin_bit_cast(vec16, c), reinterpret_cast<vec16*>(p));
+}
+
+__device__ __forceinline__ cx cmul(cx a, cx b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+// c + a*b
+__device__ __forceinline__ cx cfma(cx a, cx b, cx c) {
+  return {fma(a.x, b.x, fma(-a.y, b.y, c.x)), fma(a.x, b.y, fma(a.y, b.x, c.y))};
+}
+// c + a*conj(b)
+__device__ __forceinline__ cx cfma_conj(cx a, cx b, cx c) {
+  return {fma(a.x, b.x, fma(a.y, b.y, c.x)), fma(a.y, b.x, fma(-a.x, b.y, c.y))};
+}
+__device__ __forceinline__ cx cadd(cx a, cx b) { return {a.x + b.x, a.y + b.y}; }
+
+__device__ __forceinline__ uint64_t insert_zero(uint64_t x, uint32_t b) {
+  const uint64_t low = x & ((1ull << b) - 1ull);
+  return ((x - low) << 1) | low;
+}
+
+template <int R>
+__device__ __forceinline__ void matvec(const mat<R>& m, cx (&x)[R]) {
+  cx y[R];
+#pragma unroll
+  for (int p = 0; p < R; ++p) {
+    cx t = cmul(m.a[p * R], x[0]);
+#pragma unroll
+    for (int q = 1; q < R; ++q) t = cfma(m.a[p * R + q], x[q], t);
+    y[p] = t;
+  }
+#pragma unroll
+  for (int p = 0; p < R; ++p) x[p] = y[p];
+}
+
+// Per-gate operation applied to one R-vector: the op kinds share every kernel skeleton.
+enum OpKind { OP_APPLY = 0, OP_REVERSE = 1, OP_REVERSE_GRAD = 2, OP_INJECT = 3,
+              OP_INJECT_FIRST = 4, OP_DENSITY = 5, OP_GRAD = 6 };
+
+constexpr bool op_two_states(int op) { return op != OP_APPLY && op != OP_DENSITY; }
+constexpr bool op_reduces(int op) { return op == OP_REVERSE_GRAD || op == OP_DENSITY || op == OP_GRAD; }
+constexpr bool op_writes_f(int op) { return op == OP_APPLY || op == OP_REVERSE || op == OP_REVERSE_GRAD; }
+constexpr bool op_writes_b(int op) {
+  return op == OP_REVERSE || op == OP_REVERSE_GRAD || op == OP_INJECT || op == OP_INJECT_FIRST;
+}
+constexpr bool op_reads_b(int op) {
+  return op == OP_REVERSE || op == OP_REVERSE_GRAD || op == OP_INJECT || op == OP_GRAD;
+}
+
+// The math of each op on one canonical R-vector (f = first state, b = second state).
+//   APPLY:        f <- A f                                  (q1gate/q2gate, pr.cu:513-646)
+//   REVERSE[_GRAD]: f <- A f; [acc[pR+q] += b[p] f[q]]; b <- B b   (circuit.rs:280-392)
+//   INJECT[_FIRST]: b <- [b +] A (2 conj f)                 (circuit.rs:393-420)
+//   DENSITY:      acc[pR+q] += f[p] conj(f[q])              (pr.cu:689-837)
+//   GRAD:         acc[pR+q] += b[p] f[q]                    (pr.cu:202-354)
+template <int OP, int R>
+__device__ __forceinline__ void op_vector(const mat<R>& A, const mat<R>& B, cx (&f)[R],
+                                          cx (&b)[R], cx* acc) {
+  if constexpr (OP == OP_APPLY) {
+    matvec<R>(A, f);
+  } else if constexpr (OP == OP_REVERSE || OP == OP_REVERSE_GRAD) {
+    matvec<R>(A, f);
+    if constexpr (OP == OP_REVERSE_GRAD) {
+#pragma unroll
+      for (int p = 0; p < R; ++p)
+#pragma unroll
+        for (int q = 0; q < R; ++q) acc[p * R + q] = cfma(b[p], f[q], acc[p * R + q]);
+    }
+    matvec<R>(B, b);
+  } else if constexpr (OP == OP_INJECT || OP == OP_INJECT_FIRST) {
+    cx t[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) t[q] = {2 * f[q].x, -2 * f[q].y};
+    matvec<R>(A, t);
+#pragma unroll
+    for (int p = 0; p < R; ++p) b[p] = (OP == OP_INJECT) ? cadd(b[p], t[p]) : t[p];
+  } else if constexpr (OP == OP_DENSITY) {
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int q = 0; q < R; ++q) acc[p * R + q] = cfma_conj(f[p], f[q], acc[p * R + q]);
+  } else {  // OP_GRAD
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int q = 0; q < R; ++q) acc[p * R + q] = cfma(b[p], f[q], acc[p * R + q]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Block reduction of K complex accumulators → one RED-wide partial per block.
+// ---------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void block_reduce_store(cx (&acc)[K], cx* __restrict__ out) {
+  __shared__ cx red[BLOCK / 64][K];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    real x = acc[k].x, y = acc[k].y;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      x += __shfl_xor(x, o, 64);
+      y += __shfl_xor(y, o, 64);
+    }
+    if (lane == 0) red[wave][k] = {x, y};
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < RED) {
+    cx s = {0, 0};
+    if (t < K) {
+      s = red[0][t];
+#pragma unroll
+      for (int w = 1; w < BLOCK / 64; ++w) s = cadd(s, red[w][t]);
+    }
+    out[t] = s;  // K < RED: the unused tail of the partial is written as zeros
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// DIRECT family: row layouts.  MODE 0: every target bit is a chunk-index bit >= LOWBITS
+// (rows are whole chunks, each row a contiguous stream).  MODE 1: (VEC == 2) qubit 0 is a
+// target and it is the row's LOW index bit (q1 target, or q2 pos1).  MODE 2: (q2) qubit 0 is
+// pos2, the row's HIGH bit.  Row r of a q2 item is (P2, P1) = (r >> 1, r & 1), as in
+// primitives.cu:596-597.
+// ---------------------------------------------------------------------------------------
+struct geo {
+  uint64_t items;  // work items (one R-vector group of chunks each)
+  uint64_t sa;     // chunk stride of row bit A (q1: the target; q2 MODE 0: pos2; MODE 1/2: hi)
+  uint64_t sb;     // chunk stride of row bit B (q2 MODE 0: pos1)
+  uint32_t lo;     // chunk bit positions for zero insertion (lower first)
+  uint32_t hi;
+  uint32_t it;     // items per thread (block-contiguous iteration)
+};
+
+template <int R, int MODE>
+struct rows {
+  static constexpr int NC = (MODE == 0) ? R : R / 2;  // chunks per item (per state)
+  static constexpr int G = (MODE == 0) ? VEC : 1;     // independent R-vectors per item
+
+  __device__ static __forceinline__ void chunks(const geo& g, uint64_t i, uint64_t (&c)[NC]) {
+    if constexpr (R == 2 && MODE == 0) {
+      c[0] = insert_zero(i, g.lo);
+      c[1] = c[0] + g.sa;
+    } else if constexpr (R == 2) {
+      c[0] = i;
+    } else if constexpr (MODE == 0) {
+      const uint64_t b = insert_zero(insert_zero(i, g.lo), g.hi);
+      c[0] = b;
+      c[1] = b + g.sb;
+      c[2] = b + g.sa;
+      c[3] = b + g.sa + g.sb;
+    } else {
+      c[0] = insert_zero(i, g.hi);
+      c[1] = c[0] + g.sa;
+    }
+  }
+  __device__ static __forceinline__ void split(const chunk (&ch)[NC], cx (&x)[G][R]) {
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[v][r] = ch[r].v[v];
+    } else if constexpr (R == 2) {
+      x[0][0] = ch[0].v[0];
+      x[0][1] = ch[0].v[VEC - 1];
+    } else if constexpr (MODE == 1) {  // chunk = P2, lane = P1
+      x[0][0] = ch[0].v[0];
+      x[0][1] = ch[0].v[VEC - 1];
+      x[0][2] = ch[1].v[0];
+      x[0][3] = ch[1].v[VEC - 1];
+    } else {  // chunk = P1, lane = P2
+      x[0][0] = ch[0].v[0];
+      x[0][1] = ch[1].v[0];
+      x[0][2] = ch[0].v[VEC - 1];
+      x[0][3] = ch[1].v[VEC - 1];
+    }
+  }
+  __device__ static __forceinline__ void merge(const cx (&x)[G][R], chunk (&ch)[NC]) {
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int r = 0; r < R; ++r) ch[r].v[v] = x[v][r];
+    } else if constexpr (R == 2) {
+      ch[0].v[0] = x[0][0];
+      ch[0].v[VEC - 1] = x[0][1];
+    } else if constexpr (MODE == 1) {
+      ch[0].v[0] = x[0][0];
+      ch[0].v[VEC - 1] = x[0][1];
+      ch[1].v[0] = x[0][2];
+      ch[1].v[VEC - 1] = x[0][3];
+    } else {
+      ch[0].v[0] = x[0][0];
+      ch[1].v[0] = x[0][1];
+      ch[0].v[VEC - 1] = x[0][2];
+      ch[1].v[VEC - 1] = x[0][3];
+    }
+  }
+};
+
+// One kernel skeleton for every op of the direct family.  Block b owns the items
+// [b*BLOCK*it, (b+1)*BLOCK*it); each step keeps U items (U*NC chunks per state) in flight.
+template <int OP, int R, int MODE, int U>
+__global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                  mat<R> A, mat<R> B, geo g,
+                                                  cx* __restrict__ partials) {
+  using L = rows<R, MODE>;
+  constexpr int NACC = op_reduces(OP) ? R * R : 1;
+  cx acc[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) acc[k] = {0, 0};
+  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  for (uint32_t step = 0; step < g.it; step += U) {
+    uint64_t c[U][L::NC];
+    chunk fc[U][L::NC], bc[U][L::NC];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
+      ok[u] = (step + u < g.it) && i < g.items;
+      L::chunks(g, ok[u] ? i : 0, c[u]);
+      if (ok[u]) {
+#pragma unroll
+        for (int k = 0; k < L::NC; ++k) {
+          fc[u][k] = ldc(f + c[u][k]);
+          if constexpr (op_reads_b(OP)) bc[u][k] = ldc(b + c[u][k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      cx fx[L::G][R], bx[L::G][R];
+      L::split(fc[u], fx);
+      if constexpr (op_reads_b(OP)) L::split(bc[u], bx);
+#pragma unroll
+      for (int gg = 0; gg < L::G; ++gg) op_vector<OP, R>(A, B, fx[gg], bx[gg], acc);
+      if constexpr (op_writes_f(OP)) {
+        L::merge(fx, fc[u]);
+#pragma unroll
+        for (int k = 0; k < L::NC; ++k) stc(f + c[u][k], fc[u][k]);
+      }
+      if constexpr (op_writes_b(OP)) {
+        L::merge(bx, bc[u]);
+#pragma unroll
+        for (int k = 0; k < L::NC; ++k) stc(b + c[u][k], bc[u][k]);
+      }
+    }
+  }
+  if constexpr (op_reduces(OP)) block_reduce_store<NACC>(acc, partials + (uint64_t)blockIdx.x * RED);
+}
+
+// ---------------------------------------------------------------------------------------
+// TILE family: a workgroup stages a tile of TB = BLOCK*K contiguous... chunks of each state in
+// LDS.  Tile-local chunk index c (0..TB): low `l` bits contiguous in HBM, the next `h` bits
+// are "row" bits placed at global chunk bits hb[0] < hb[1] (far targets).  Every wave
+// instruction of the load/store moves 64 consecutive chunks (l >= 8).  The gate acts on
+// tile-local amplitude bits t1 (pos1 / q1 target) and t2 (pos2).
+// ---------------------------------------------------------------------------------------
+struct tgeo {
+  uint64_t ntiles;
+  uint32_t tpb;    // tiles per block (block-contiguous)
+  uint32_t l;      // contiguous low chunk bits of a tile
+  uint32_t h;      // row bits (0..2)
+  uint32_t hb0, hb1;  // global chunk bit of row bit 0 / 1
+  uint32_t t1, t2;    // tile-local amplitude bits of the gate's index bits 0 (pos1) and 1 (pos2)
+};
+
+__device__ __forceinline__ uint64_t tile_base(const tgeo& tg, uint64_t tile) {
+  uint64_t base = tile << tg.l;
+  if (tg.h > 0) base = insert_zero(base, tg.hb0);
+  if (tg.h > 1) base = insert_zero(base, tg.hb1);
+  return base;
+}
+__device__ __forceinline__ uint64_t tile_chunk(const tgeo& tg, uint64_t base, uint32_t c) {
+  uint64_t g = base + (c & ((1u << tg.l) - 1u));
+  if (tg.h > 0) g += (uint64_t)((c >> tg.l) & 1u) << tg.hb0;
+  if (tg.h > 1) g += (uint64_t)((c >> (tg.l + 1)) & 1u) << tg.hb1;
+  return g;
+}
+
+template <int OP, int R, int K>
+__global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                mat<R> A, mat<R> B, tgeo tg,
+                                                cx* __restrict__ partials) {
+  constexpr int TB = BLOCK * K;                 // chunks per state per tile
+  constexpr int NS = op_two_states(OP) ? 2 : 1;
+  __shared__ chunk lds[NS][TB];
+  constexpr int NACC = op_reduces(OP) ? R * R : 1;
+  cx acc[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) acc[k] = {0, 0};
+  const uint32_t t = threadIdx.x;
+  const uint32_t tc = 1u << (tg.l + tg.h);     // chunks per tile (== TB except tiny states)
+  const uint32_t ng = (tc * VEC) / R;          // gate groups per tile
+  const uint32_t lo_t = tg.t1 < tg.t2 ? tg.t1 : tg.t2;
+  const uint32_t hi_t = tg.t1 < tg.t2 ? tg.t2 : tg.t1;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * tg.tpb;
+  for (uint32_t tt = 0; tt < tg.tpb; ++tt) {
+    const uint64_t tile = tile0 + tt;
+    if (tile >= tg.ntiles) break;
+    const uint64_t base = tile_base(tg, tile);
+    uint64_t gi[K];
+    chunk rf[K], rb[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k * BLOCK + t >= tc) break;
+      gi[k] = tile_chunk(tg, base, k * BLOCK + t);
+      rf[k] = ldc(f + gi[k]);
+      if constexpr (op_reads_b(OP)) rb[k] = ldc(b + gi[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k * BLOCK + t >= tc) break;
+      lds[0][k * BLOCK + t] = rf[k];
+      if constexpr (op_reads_b(OP)) lds[NS - 1][k * BLOCK + t] = rb[k];
+    }
+    __syncthreads();
+    cx* lf = reinterpret_cast<cx*>(&lds[0][0]);
+    cx* lb = reinterpret_cast<cx*>(&lds[NS - 1][0]);
+    for (uint32_t grp = t; grp < ng; grp += BLOCK) {
+      uint32_t a0;
+      uint32_t off[R];
+      if constexpr (R == 2) {
+        a0 = (uint32_t)insert_zero(grp, tg.t1);
+        off[0] = 0;
+        off[1] = 1u << tg.t1;
+      } else {
+        a0 = (uint32_t)insert_zero(insert_zero(grp, lo_t), hi_t);
+        off[0] = 0;
+        off[1] = 1u << tg.t1;
+        off[2] = 1u << tg.t2;
+        off[3] = off[1] + off[2];
+      }
+      cx fx[R], bx[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        fx[r] = lf[a0 + off[r]];
+        if constexpr (op_reads_b(OP)) bx[r] = lb[a0 + off[r]];
+      }
+      op_vector<OP, R>(A, B, fx, bx, acc);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (op_writes_f(OP)) lf[a0 + off[r]] = fx[r];
+        if constexpr (op_writes_b(OP)) lb[a0 + off[r]] = bx[r];
+      }
+    }
+    if constexpr (op_writes_f(OP) || op_writes_b(OP)) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (k * BLOCK + t >= tc) break;
+        if constexpr (op_writes_f(OP)) stc(f + gi[k], lds[0][k * BLOCK + t]);
+        if constexpr (op_writes_b(OP)) stc(b + gi[k], lds[NS - 1][k * BLOCK + t]);
+      }
+    }
+    __syncthreads();  // the next tile overwrites lds
+  }
+  if constexpr (op_reduces(OP)) block_reduce_store<NACC>(acc, partials + (uint64_t)blockIdx.x * RED);
+}
+
+// ---------------------------------------------------------------------------------------
+// Diagonal two-qubit gates: purely elementwise over chunks, every position pair is a fully
+// contiguous stream.  k = 2 bit(i,pos2) + bit(i,pos1)  (primitives.cu:649-672, 398-452).
+//   DIAG_APPLY: s <- d s;  DIAG_REVERSE[_GRAD]: f <- dc f; [G[k] += b f]; b <- d b;
+//   DIAG_GRAD: G[k] += b f.
+// ---------------------------------------------------------------------------------------
+enum DiagOp { DIAG_APPLY = 0, DIAG_REVERSE = 1, DIAG_REVERSE_GRAD = 2, DIAG_GRAD = 3 };
+
+__device__ __forceinline__ cx pick4(const diag4& d, uint32_t k) {
+  const cx lo = (k & 1) ? d.a[1] : d.a[0];
+  const cx hi = (k & 1) ? d.a[3] : d.a[2];
+  return (k & 2) ? hi : lo;
+}
+
+struct dgeo {
+  uint64_t nchunks;
+  uint32_t it;
+  uint32_t p2, p1;
+};
+
+template <int OP, int U>
+__global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                diag4 dc, diag4 d, dgeo g,
+                                                cx* __restrict__ partials) {
+  constexpr bool RED_ = (OP == DIAG_REVERSE_GRAD || OP == DIAG_GRAD);
+  constexpr bool TWO = (OP != DIAG_APPLY);
+  cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  for (uint32_t step = 0; step < g.it; step += U) {
+    chunk fc[U], bc[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
+      ok[u] = (step + u < g.it) && i < g.nchunks;
+      if (ok[u]) {
+        fc[u] = ldc(f + i);
+        if constexpr (TWO) bc[u] = ldc(b + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const uint64_t a = i * VEC + v;
+        const uint32_t k = (uint32_t)(((a >> g.p2) & 1) << 1 | ((a >> g.p1) & 1));
+        if constexpr (OP == DIAG_APPLY) {
+          fc[u].v[v] = cmul(pick4(d, k), fc[u].v[v]);
+        } else if constexpr (OP == DIAG_GRAD) {
+          const cx prod = cmul(bc[u].v[v], fc[u].v[v]);
+#pragma unroll
+          for (uint32_t kk = 0; kk < 4; ++kk) acc[kk] = cadd(acc[kk], (k == kk) ? prod : cx{0, 0});
+        } else {
+          const cx fv = cmul(pick4(dc, k), fc[u].v[v]);
+          if constexpr (OP == DIAG_REVERSE_GRAD) {
+            const cx prod = cmul(bc[u].v[v], fv);
+#pragma unroll
+            for (uint32_t kk = 0; kk < 4; ++kk)
+              acc[kk] = cadd(acc[kk], (k == kk) ? prod : cx{0, 0});
+          }
+          fc[u].v[v] = fv;
+          bc[u].v[v] = cmul(pick4(d, k), bc[u].v[v]);
+        }
+      }
+      if constexpr (OP != DIAG_GRAD) stc(f + i, fc[u]);
+      if constexpr (OP == DIAG_REVERSE || OP == DIAG_REVERSE_GRAD) stc(b + i, bc[u]);
+    }
+  }
+  if constexpr (RED_) block_reduce_store<4>(acc, partials + (uint64_t)blockIdx.x * RED);
+}
+
+// ---------------------------------------------------------------------------------------
+// Partial-sum finalize: one block per pending reduction slot, fixed summation order.
+// dst[slot_dst[s]*RED + k] (+)= sum_b partials[s][b][k].
+// ---------------------------------------------------------------------------------------
+constexpr int FIN_MAX = 32;
+struct fin_table {
+  uint32_t dst[FIN_MAX];
+};
+
+__global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ partials,
+                                                    uint64_t slot_stride, uint32_t nblocks,
+                                                    fin_table tab, cx* __restrict__ dst,
+                                                    int accumulate) {
+  const cx* p = partials + (uint64_t)blockIdx.x * slot_stride;
+  cx acc[RED];
+#pragma unroll
+  for (int k = 0; k < RED; ++k) acc[k] = {0, 0};
+  for (uint32_t blk = threadIdx.x; blk < nblocks; blk += BLOCK) {
+#pragma unroll
+    for (int k = 0; k < RED; ++k) acc[k] = cadd(acc[k], p[(uint64_t)blk * RED + k]);
+  }
+  __shared__ cx out[RED];
+  block_reduce_store<RED>(acc, out);
+  __syncthreads();
+  if (threadIdx.x < RED) {
+    cx* d = dst + (uint64_t)tab.dst[blockIdx.x] * RED + threadIdx.x;
+    *d = accumulate ? cadd(*d, out[threadIdx.x]) : out[threadIdx.x];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Elementwise state kernels (primitives.cu:176-187, 879-939).
+// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>
+// ---------------------------------------------------------------------------------------
+template <int OP>
+__global__ __launch_bounds__(BLOCK) void k_elementwise(const cx* __restrict__ src,
+                                                       cx* __restrict__ dst, uint64_t n,
+                                                       uint32_t it) {
+  const uint64_t nch = n / VEC;
+  const chunk* s = reinterpret_cast<const chunk*>(src);
+  chunk* d = reinterpret_cast<chunk*>(dst);
+  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * it + threadIdx.x;
+  for (uint32_t step = 0; step < it; ++step) {
+    const uint64_t i = start + (uint64_t)step * BLOCK;
+    if (i >= nch) break;
+    chunk a;
+    if constexpr (OP == 3) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) a.v[v] = (i == 0 && v == 0) ? cx{1, 0} : cx{0, 0};
+    } else {
+      a = ldc(s + i);
+    }
+    if constexpr (OP == 1) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) a.v[v] = {2 * a.v[v].x, -2 * a.v[v].y};
+    } else if constexpr (OP == 2) {
+      const chunk o = ldc(d + i);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) a.v[v] = cadd(o.v[v], a.v[v]);
+    }
+    stc(d + i, a);
+  }
+  // n < VEC (a 0-qubit state in f32): scalar tail
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (uint64_t k = nch * VEC; k < n; ++k) {
+      cx a = (OP == 3) ? cx{k == 0 ? (real)1 : (real)0, 0} : src[k];
+      if constexpr (OP == 1) a = {2 * a.x, -2 * a.y};
+      if constexpr (OP == 2) a = cadd(dst[k], a);
+      dst[k] = a;
+    }
+  }
+}
+
+}  // namespace qdc

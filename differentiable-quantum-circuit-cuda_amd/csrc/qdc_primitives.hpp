@@ -1,0 +1,264 @@
+// qdc_primitives.hpp — the 18 reference C-ABI entry points (src/primitives_bind.rs:15-119,
+// implemented for CUDA in src/primitives.cu:141-953) on the HIP kernels.
+//
+// All calls share one process-wide context on the device that was current at first use:
+// one non-blocking stream, ordered exactly like the reference's legacy default stream; host
+// results (copies, densities, gradients) synchronise it.  A mutex makes concurrent callers
+// safe (the reference's are not, README.md:13).
+#pragma once
+
+#include "qdc_device.hpp"
+
+namespace qdc {
+
+inline std::mutex& abi_mutex() {
+  static std::mutex m;
+  return m;
+}
+
+inline const char* abi_ctx(Ctx*& out) {
+  static Ctx* ctx = nullptr;
+  if (!ctx) {
+    int dev = 0;
+    QDC_HIP(hipGetDevice(&dev));
+    Ctx* c = new Ctx();
+    const char* e = c->init(dev);
+    if (e) {
+      delete c;
+      return e;
+    }
+    ctx = c;
+  }
+  out = ctx;
+  return nullptr;
+}
+
+inline const char* check_n(size_t n) {
+  if (n > 40) return fail("qubits_number %zu is out of the supported range (<= 40).", n);
+  return nullptr;
+}
+
+// one reduction → host `out[0..K)` += result (the reference's `+=`, primitives.cu:281-288)
+inline const char* abi_finish_reduction(Ctx& c, qdc_complex* out, int K) {
+  QDC_TRY(c.flush());
+  QDC_HIP(hipMemcpyAsync(c.host_results, c.results, sizeof(cx) * RED, hipMemcpyDeviceToHost,
+                         c.stream));
+  QDC_HIP(hipStreamSynchronize(c.stream));
+  for (int k = 0; k < K; ++k) {
+    out[k].re += c.host_results[k].x;
+    out[k].im += c.host_results[k].y;
+  }
+  return nullptr;
+}
+
+}  // namespace qdc
+
+#define QDC_ABI_BEGIN                                   \
+  std::lock_guard<std::mutex> qdc_lock_(qdc::abi_mutex()); \
+  qdc::Ctx* ctxp = nullptr;                             \
+  QDC_TRY(qdc::abi_ctx(ctxp));                          \
+  qdc::Ctx& ctx = *ctxp;
+
+#define QDC_VOID(expr)                                                  \
+  do {                                                                  \
+    const char* qdc_v_ = (expr);                                        \
+    if (qdc_v_) fprintf(stderr, "qdc: %s\n", qdc_v_);                   \
+  } while (0)
+
+static const char* set2standard_impl(qdc_complex* state, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  return qdc::set_standard(ctx, reinterpret_cast<qdc::cx*>(state), (uint32_t)n);
+}
+
+static const char* check_q2(size_t pos2, size_t pos1, size_t n) {
+  if (pos1 == pos2) return qdc::fail("pos1 and pos2 must be different.");
+  if (pos1 >= n) return qdc::fail("pos1 is out of the bound.");
+  if (pos2 >= n) return qdc::fail("pos2 is out of the bound.");
+  return nullptr;
+}
+
+template <int OP>
+static const char* elementwise_impl(const qdc_complex* src, qdc_complex* dst, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  return qdc::elementwise<OP>(ctx, reinterpret_cast<const qdc::cx*>(src),
+                              reinterpret_cast<qdc::cx*>(dst), (uint32_t)n);
+}
+
+extern "C" {
+
+__attribute__((visibility("default"))) void set2standard(qdc_complex* state, size_t n) {
+  QDC_VOID(set2standard_impl(state, n));
+}
+
+__attribute__((visibility("default"))) const char* get_state(qdc_complex** state, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  (void)ctx;
+  QDC_HIP(hipMalloc(reinterpret_cast<void**>(state), ((size_t)1 << n) * sizeof(qdc_complex)));
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) const char* drop_state(qdc_complex* state) {
+  QDC_ABI_BEGIN
+  QDC_HIP(hipStreamSynchronize(ctx.stream));
+  QDC_HIP(hipFree(state));
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) const char* copy_to_host(const qdc_complex* state,
+                                                                qdc_complex* host, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_HIP(hipMemcpyAsync(host, state, ((size_t)1 << n) * sizeof(qdc_complex),
+                         hipMemcpyDeviceToHost, ctx.stream));
+  QDC_HIP(hipStreamSynchronize(ctx.stream));
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) const char* set_from_host(qdc_complex* dev,
+                                                                 const qdc_complex* host,
+                                                                 size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_HIP(hipMemcpyAsync(dev, host, ((size_t)1 << n) * sizeof(qdc_complex),
+                         hipMemcpyHostToDevice, ctx.stream));
+  QDC_HIP(hipStreamSynchronize(ctx.stream));
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) const char* q1gate(qdc_complex* state,
+                                                          const qdc_complex* gate, size_t pos,
+                                                          size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  if (pos >= n) return qdc::fail("pos is out of the bound.");
+  return qdc::apply_dense<2>(ctx, reinterpret_cast<qdc::cx*>(state), qdc::to_mat<2>(gate),
+                             (uint32_t)pos, (uint32_t)pos, (uint32_t)n, "q1gate");
+}
+
+__attribute__((visibility("default"))) const char* q1gate_inv(qdc_complex* state,
+                                                              const qdc_complex* gate,
+                                                              size_t pos, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  if (pos >= n) return qdc::fail("pos is out of the bound.");
+  qdc::mat<2> inv;
+  QDC_TRY(qdc::inverse<2>(qdc::to_mat<2>(gate), inv));
+  return qdc::apply_dense<2>(ctx, reinterpret_cast<qdc::cx*>(state), inv, (uint32_t)pos,
+                             (uint32_t)pos, (uint32_t)n, "q1gate");
+}
+
+__attribute__((visibility("default"))) const char* q2gate(qdc_complex* state,
+                                                          const qdc_complex* gate, size_t pos2,
+                                                          size_t pos1, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  return qdc::apply_dense<4>(ctx, reinterpret_cast<qdc::cx*>(state), qdc::to_mat<4>(gate),
+                             (uint32_t)pos2, (uint32_t)pos1, (uint32_t)n, "q2gate");
+}
+
+__attribute__((visibility("default"))) const char* q2gate_inv(qdc_complex* state,
+                                                              const qdc_complex* gate,
+                                                              size_t pos2, size_t pos1,
+                                                              size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  qdc::mat<4> inv;
+  QDC_TRY(qdc::inverse<4>(qdc::to_mat<4>(gate), inv));
+  return qdc::apply_dense<4>(ctx, reinterpret_cast<qdc::cx*>(state), inv, (uint32_t)pos2,
+                             (uint32_t)pos1, (uint32_t)n, "q2gate");
+}
+
+__attribute__((visibility("default"))) const char* q2gate_diag(qdc_complex* state,
+                                                               const qdc_complex* gate,
+                                                               size_t pos2, size_t pos1,
+                                                               size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  return qdc::apply_diag(ctx, reinterpret_cast<qdc::cx*>(state), qdc::to_diag(gate),
+                         (uint32_t)pos2, (uint32_t)pos1, (uint32_t)n, "q2gate_diag");
+}
+
+__attribute__((visibility("default"))) const char* get_q1density(const qdc_complex* state,
+                                                                 qdc_complex* density,
+                                                                 size_t pos, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  if (pos >= n) return qdc::fail("pos is out of the bound.");
+  QDC_TRY(qdc::density<2>(ctx, reinterpret_cast<const qdc::cx*>(state), (uint32_t)pos,
+                          (uint32_t)pos, (uint32_t)n, ctx.results, 0, 0));
+  return qdc::abi_finish_reduction(ctx, density, 4);
+}
+
+__attribute__((visibility("default"))) const char* get_q2density(const qdc_complex* state,
+                                                                 qdc_complex* density,
+                                                                 size_t pos2, size_t pos1,
+                                                                 size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  QDC_TRY(qdc::density<4>(ctx, reinterpret_cast<const qdc::cx*>(state), (uint32_t)pos2,
+                          (uint32_t)pos1, (uint32_t)n, ctx.results, 0, 0));
+  return qdc::abi_finish_reduction(ctx, density, 16);
+}
+
+__attribute__((visibility("default"))) const char* q1grad(const qdc_complex* fwd,
+                                                          const qdc_complex* bwd,
+                                                          qdc_complex* grad, size_t pos,
+                                                          size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  if (pos >= n) return qdc::fail("pos out of range.");
+  QDC_TRY(qdc::grad_dense<2>(ctx, reinterpret_cast<const qdc::cx*>(fwd),
+                             reinterpret_cast<const qdc::cx*>(bwd), (uint32_t)pos, (uint32_t)pos,
+                             (uint32_t)n, ctx.results, 0, 0));
+  return qdc::abi_finish_reduction(ctx, grad, 4);
+}
+
+__attribute__((visibility("default"))) const char* q2grad(const qdc_complex* fwd,
+                                                          const qdc_complex* bwd,
+                                                          qdc_complex* grad, size_t pos2,
+                                                          size_t pos1, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  QDC_TRY(qdc::grad_dense<4>(ctx, reinterpret_cast<const qdc::cx*>(fwd),
+                             reinterpret_cast<const qdc::cx*>(bwd), (uint32_t)pos2,
+                             (uint32_t)pos1, (uint32_t)n, ctx.results, 0, 0));
+  return qdc::abi_finish_reduction(ctx, grad, 16);
+}
+
+__attribute__((visibility("default"))) const char* q2grad_diag(const qdc_complex* fwd,
+                                                               const qdc_complex* bwd,
+                                                               qdc_complex* grad, size_t pos2,
+                                                               size_t pos1, size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  QDC_TRY(check_q2(pos2, pos1, n));
+  QDC_TRY(qdc::grad_diag(ctx, reinterpret_cast<const qdc::cx*>(fwd),
+                         reinterpret_cast<const qdc::cx*>(bwd), (uint32_t)pos2, (uint32_t)pos1,
+                         (uint32_t)n, ctx.results, 0, 0));
+  return qdc::abi_finish_reduction(ctx, grad, 4);
+}
+
+__attribute__((visibility("default"))) void conj_and_double(const qdc_complex* src,
+                                                             qdc_complex* dst, size_t n) {
+  QDC_VOID(elementwise_impl<1>(src, dst, n));
+}
+
+__attribute__((visibility("default"))) void add(const qdc_complex* src, qdc_complex* dst,
+                                                size_t n) {
+  QDC_VOID(elementwise_impl<2>(src, dst, n));
+}
+
+__attribute__((visibility("default"))) void copy(const qdc_complex* src, qdc_complex* dst,
+                                                 size_t n) {
+  QDC_VOID(elementwise_impl<0>(src, dst, n));
+}
+
+}  // extern "C"

@@ -1,0 +1,378 @@
+"""quantum_differentiable_circuit — drop-in for the reference's PyO3 module of the same name
+(``src/circuit.rs:432-436``), backed by the HIP/gfx950 runtime in ``libqdc_{f32,f64}.so``.
+
+``Circuit`` reproduces ``#[pyclass] Circuit`` (``src/circuit.rs:86-430``) method for method:
+the builders, ``run``, ``forward`` and ``backward``, their argument order, their outputs
+(lists of 2-D density matrices / 1-D gate gradients) and their panic messages.  Like the
+reference there is one precision per library; the module-level ``Circuit`` uses the precision
+named by ``QDC_PRECISION`` (``f32`` default, or ``f64``), and ``Circuit32`` / ``Circuit64`` pin
+one explicitly.  Input arrays must have the build's dtype (complex64 / complex128), as PyO3's
+``PyReadonlyArray1<Complex>`` extraction demands.
+
+``QuantizedTensor`` and the ``get_q*_grad`` / ``data_transfer`` helpers mirror
+``src/quantized_tensor.rs:54-238`` over the 18-function C ABI, so the parity tests can follow
+the reference's own unit tests (``quantized_tensor.rs:400-609``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence
+
+import numpy as np
+
+from ._native import (PanicException, KernelStat, check, default_precision, load, ptr,
+                      PRECISIONS)
+
+__all__ = ["Circuit", "Circuit32", "Circuit64", "QuantizedTensor", "PanicException",
+           "get_q1_grad", "get_q2_grad", "get_q2_grad_diag", "data_transfer", "circuit_class"]
+
+# enum Instruction order (src/circuit.rs:53-68) == enum qdc_kind (include/qdc/circuit.h)
+(CONST_Q2, VAR_Q2, CONST_Q2_NONU, VAR_Q2_NONU, CONST_Q2_DIAG, VAR_Q2_DIAG, CONST_Q1,
+ CONST_Q1_NONU, VAR_Q1, VAR_Q1_NONU, Q2_DENSITY, Q1_DENSITY, DIFF_Q2_DENSITY,
+ DIFF_Q1_DENSITY) = range(14)
+MODE_RUN, MODE_FORWARD = 0, 1
+
+
+def _array1(x, dtype, what):
+    """PyReadonlyArray1<Complex> extraction: an ndarray of exactly this dtype and ndim 1."""
+    if not isinstance(x, np.ndarray) or x.dtype != dtype or x.ndim != 1:
+        raise TypeError(f"argument '{what}': expected a 1-D numpy array of {np.dtype(dtype)}")
+    return x
+
+
+def _array2(x, dtype, what):
+    if not isinstance(x, np.ndarray) or x.dtype != dtype or x.ndim != 2:
+        raise TypeError(f"argument '{what}': expected a 2-D numpy array of {np.dtype(dtype)}")
+    return x
+
+
+def _flatten(arrays, dtype, what, msg):
+    """Concatenate host buffers for the C ABI; as_slice() panics on non-contiguous input."""
+    lens = np.fromiter((a.size for a in arrays), dtype=np.uintp, count=len(arrays))
+    for a in arrays:
+        if not a.flags.c_contiguous:
+            raise PanicException(msg)
+    flat = np.concatenate([a.reshape(-1) for a in arrays]) if arrays else np.zeros(1, dtype)
+    return np.ascontiguousarray(flat, dtype=dtype), lens if len(arrays) else np.zeros(1, np.uintp)
+
+
+class _CircuitBase:
+    _precision = "f32"
+
+    def __init__(self, qubits_number: int):
+        self._lib = load(self._precision)
+        self._dtype = np.dtype(PRECISIONS[self._precision])
+        h = C.c_void_p()
+        check(self._lib.qdc_circuit_new(C.byref(h), int(qubits_number)))
+        self._h = h
+        self._n = int(qubits_number)
+        self._kinds = []  # instruction kinds, for splitting the flat outputs
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.qdc_circuit_free(h)
+            self._h = None
+
+    @property
+    def qubits_number(self) -> int:
+        return self._n
+
+    @property
+    def dtype(self):
+        return self._dtype
+
+    # --- circuit.rs:104-106 -----------------------------------------------------------
+    def set_state_from_vector(self, vector: np.ndarray) -> None:
+        v = _array1(vector, self._dtype, "vector")
+        if not v.flags.c_contiguous:
+            raise PanicException("called `Option::unwrap()` on a `None` value")
+        check(self._lib.qdc_circuit_set_state_from_vector(self._h, ptr(v), v.size))
+
+    # --- builders, circuit.rs:108-162 -------------------------------------------------
+    def _push(self, kind, a, b=0):
+        if a < 0 or b < 0:
+            raise OverflowError("can't convert negative int to unsigned")
+        check(self._lib.qdc_circuit_push(self._h, kind, int(a), int(b)))
+        self._kinds.append(kind)
+
+    def add_q2_const_gate(self, pos2: int, pos1: int): self._push(CONST_Q2, pos2, pos1)
+    def add_q2_const_gate_diag(self, pos2: int, pos1: int): self._push(CONST_Q2_DIAG, pos2, pos1)
+    def add_q2_const_gate_nonu(self, pos2: int, pos1: int): self._push(CONST_Q2_NONU, pos2, pos1)
+    def add_q2_var_gate(self, pos2: int, pos1: int): self._push(VAR_Q2, pos2, pos1)
+    def add_q2_var_gate_diag(self, pos2: int, pos1: int): self._push(VAR_Q2_DIAG, pos2, pos1)
+    def add_q2_var_gate_nonu(self, pos2: int, pos1: int): self._push(VAR_Q2_NONU, pos2, pos1)
+    def add_q1_const_gate(self, pos: int): self._push(CONST_Q1, pos)
+    def add_q1_const_gate_nonu(self, pos: int): self._push(CONST_Q1_NONU, pos)
+    def add_q1_var_gate(self, pos: int): self._push(VAR_Q1, pos)
+    def add_q1_var_gate_nonu(self, pos: int): self._push(VAR_Q1_NONU, pos)
+    def get_q2_dens_op(self, pos2: int, pos1: int): self._push(Q2_DENSITY, pos2, pos1)
+    def get_q1_dens_op(self, pos: int): self._push(Q1_DENSITY, pos)
+    def get_q2_dens_op_with_grad(self, pos2: int, pos1: int): self._push(DIFF_Q2_DENSITY, pos2, pos1)
+    def get_q1_dens_op_with_grad(self, pos: int): self._push(DIFF_Q1_DENSITY, pos)
+
+    def __len__(self):
+        return int(self._lib.qdc_circuit_len(self._h))
+
+    # --- execution ---------------------------------------------------------------------
+    def _gates(self, gates: Sequence[np.ndarray], what: str):
+        gates = [_array1(g, self._dtype, what) for g in gates]
+        return _flatten(gates, self._dtype, what, "Gate is not contiguous.")
+
+    def run(self, const_gates: List[np.ndarray], var_gates: List[np.ndarray]) -> List[np.ndarray]:
+        """circuit.rs:164-212: every density matrix, in instruction order."""
+        return self._exec(MODE_RUN, const_gates, var_gates)
+
+    def forward(self, const_gates: List[np.ndarray], var_gates: List[np.ndarray]) -> List[np.ndarray]:
+        """circuit.rs:214-264: the Diff* density matrices, in instruction order."""
+        return self._exec(MODE_FORWARD, const_gates, var_gates)
+
+    def _exec(self, mode, const_gates, var_gates):
+        cf, cl = self._gates(const_gates, "const_gates")
+        vf, vl = self._gates(var_gates, "var_gates")
+        size = int(self._lib.qdc_circuit_output_size(self._h, mode))
+        out = np.empty(max(size, 1), dtype=self._dtype)
+        check(self._lib.qdc_circuit_execute(self._h, mode, ptr(cf), ptr(cl), len(const_gates),
+                                             ptr(vf), ptr(vl), len(var_gates), ptr(out)))
+        res, o = [], 0
+        for is_q1 in self._out_kinds(mode):
+            k = 2 if is_q1 else 4
+            res.append(out[o:o + k * k].reshape(k, k).copy())
+            o += k * k
+        assert o == size
+        return res
+
+    def backward(self, grads_wrt_density: List[np.ndarray], const_gates: List[np.ndarray],
+                 var_gates: List[np.ndarray]) -> List[np.ndarray]:
+        """circuit.rs:266-429: gradients of the variable gates, forward order."""
+        dens = [_array2(g, self._dtype, "grads_wrt_density") for g in grads_wrt_density]
+        df, dl = _flatten(dens, self._dtype, "grads_wrt_density", "Gradient is not contiguous.")
+        cf, cl = self._gates(const_gates, "const_gates")
+        vf, vl = self._gates(var_gates, "var_gates")
+        size = int(self._lib.qdc_circuit_grad_size(self._h))
+        out = np.empty(max(size, 1), dtype=self._dtype)
+        check(self._lib.qdc_circuit_backward(self._h, ptr(df), ptr(dl), len(dens), ptr(cf),
+                                              ptr(cl), len(const_gates), ptr(vf), ptr(vl),
+                                              len(var_gates), ptr(out)))
+        res, o = [], 0
+        for w in self._var_widths():
+            res.append(out[o:o + w].copy())
+            o += w
+        return res
+
+    # --- instruction metadata (kept on the Python side for output splitting) -----------
+    def _out_kinds(self, mode):
+        return [k in (Q1_DENSITY, DIFF_Q1_DENSITY) for k in self._kinds
+                if k in (DIFF_Q1_DENSITY, DIFF_Q2_DENSITY)
+                or (mode == MODE_RUN and k in (Q1_DENSITY, Q2_DENSITY))]
+
+    def _var_widths(self):
+        return [16 if k in (VAR_Q2, VAR_Q2_NONU) else 4 for k in self._kinds
+                if k in (VAR_Q1, VAR_Q1_NONU, VAR_Q2, VAR_Q2_NONU, VAR_Q2_DIAG)]
+
+    # --- extras (not in the reference's Python surface) --------------------------------
+    def get_state(self, which: int = 0) -> np.ndarray:
+        """Copy of the forward (0), initial (1) or backward (2) device state."""
+        out = np.empty(1 << self._n, dtype=self._dtype)
+        check(self._lib.qdc_circuit_get_state(self._h, which, ptr(out), out.size))
+        return out
+
+    def synchronize(self):
+        check(self._lib.qdc_circuit_sync(self._h))
+
+    def profile(self, on: bool):
+        check(self._lib.qdc_circuit_profile(self._h, 1 if on else 0))
+
+    def profile_collect(self):
+        cap = 64
+        buf = (KernelStat * cap)()
+        k = int(self._lib.qdc_circuit_profile_collect(self._h, buf, cap))
+        return {buf[i].name.decode(): {"launches": int(buf[i].launches),
+                                        "total_ms": float(buf[i].total_ms),
+                                        "algo_bytes": float(buf[i].algo_bytes)}
+                for i in range(min(k, cap))}
+
+
+class Circuit32(_CircuitBase):
+    """Single-precision build (complex64), like `maturin develop --release`."""
+    _precision = "f32"
+
+
+class Circuit64(_CircuitBase):
+    """Double-precision build (complex128), like `maturin develop --features "f64"`."""
+    _precision = "f64"
+
+
+def circuit_class(precision: str | None = None):
+    p = precision or default_precision()
+    return Circuit64 if p == "f64" else Circuit32
+
+
+Circuit = circuit_class()
+
+
+# ---------------------------------------------------------------------------------------
+# QuantizedTensor (src/quantized_tensor.rs:54-238) over the 18-function C ABI
+# ---------------------------------------------------------------------------------------
+class QuantizedTensor:
+    """A device state of 2^n amplitudes owned by this object (RAII like the Rust struct)."""
+
+    def __init__(self, qubits_number: int, precision: str | None = None, _ptr=None):
+        self._precision = precision or default_precision()
+        self._lib = load(self._precision)
+        self.dtype = np.dtype(PRECISIONS[self._precision])
+        self.qubits_number = int(qubits_number)
+        if _ptr is None:
+            p = C.c_void_p()
+            check(self._lib.get_state(C.byref(p), self.qubits_number))
+            _ptr = p
+        self._p = _ptr
+
+    @classmethod
+    def new_standard(cls, qubits_number, precision=None):
+        t = cls(qubits_number, precision)
+        t._lib.set2standard(t._p, t.qubits_number)
+        return t
+
+    @classmethod
+    def new_from_host(cls, state: np.ndarray, precision=None):
+        size = state.size
+        if size == 0 or size & (size - 1):
+            raise PanicException("State size is not a power of 2.")
+        t = cls(size.bit_length() - 1, precision)
+        t.set_from_host(state)
+        return t
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            check(self._lib.drop_state(p))
+            self._p = None
+
+    def _host(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        return a
+
+    def set_from_host(self, state):
+        s = self._host(state)
+        if s.size != (1 << self.qubits_number):
+            raise PanicException("Size of the given state does not match the size of the tensor.")
+        check(self._lib.set_from_host(self._p, ptr(s), self.qubits_number))
+
+    def get_cpu_state_copy(self) -> np.ndarray:
+        out = np.empty(1 << self.qubits_number, dtype=self.dtype)
+        check(self._lib.copy_to_host(self._p, ptr(out), self.qubits_number))
+        return out
+
+    def clone(self):
+        t = QuantizedTensor(self.qubits_number, self._precision)
+        self._lib.copy(self._p, t._p, self.qubits_number)
+        return t
+
+    def conj_and_double(self):
+        t = QuantizedTensor(self.qubits_number, self._precision)
+        self._lib.conj_and_double(self._p, t._p, self.qubits_number)
+        return t
+
+    def add(self, other: "QuantizedTensor"):
+        if other.qubits_number != self.qubits_number:
+            raise PanicException("Tensors have diferent sizes.")
+        self._lib.add(other._p, self._p, self.qubits_number)
+
+    def _gate(self, gate, want):
+        g = self._host(gate).reshape(-1)
+        if g.size != want:
+            raise PanicException("Incorrect len of the gate's buffer.")
+        return g
+
+    def _pos1(self, pos):
+        if pos >= self.qubits_number:
+            raise PanicException("pos is out of the bound.")
+
+    def _pos2(self, pos2, pos1):
+        if pos1 == pos2:
+            raise PanicException("pos1 and pos2 must be different.")
+        if pos1 >= self.qubits_number:
+            raise PanicException("pos1 is out of the bound.")
+        if pos2 >= self.qubits_number:
+            raise PanicException("pos2 is out of the bound.")
+
+    def apply_q1_gate(self, gate, pos):
+        g = self._gate(gate, 4)
+        self._pos1(pos)
+        check(self._lib.q1gate(self._p, ptr(g), pos, self.qubits_number))
+
+    def apply_q1_gate_inv(self, gate, pos):
+        g = self._gate(gate, 4)
+        self._pos1(pos)
+        check(self._lib.q1gate_inv(self._p, ptr(g), pos, self.qubits_number))
+
+    def apply_q1_gate_tr(self, gate, pos):
+        self.apply_q1_gate(self._host(gate).reshape(2, 2).T.reshape(-1), pos)
+
+    def apply_q1_gate_conj_tr(self, gate, pos):
+        self.apply_q1_gate(self._host(gate).reshape(2, 2).T.conj().reshape(-1), pos)
+
+    def apply_q2_gate(self, gate, pos2, pos1):
+        g = self._gate(gate, 16)
+        self._pos2(pos2, pos1)
+        check(self._lib.q2gate(self._p, ptr(g), pos2, pos1, self.qubits_number))
+
+    def apply_q2_gate_inv(self, gate, pos2, pos1):
+        g = self._gate(gate, 16)
+        self._pos2(pos2, pos1)
+        check(self._lib.q2gate_inv(self._p, ptr(g), pos2, pos1, self.qubits_number))
+
+    def apply_q2_gate_tr(self, gate, pos2, pos1):
+        self.apply_q2_gate(self._host(gate).reshape(4, 4).T.reshape(-1), pos2, pos1)
+
+    def apply_q2_gate_conj_tr(self, gate, pos2, pos1):
+        self.apply_q2_gate(self._host(gate).reshape(4, 4).T.conj().reshape(-1), pos2, pos1)
+
+    def apply_q2_gate_diag(self, gate, pos2, pos1):
+        g = self._gate(gate, 4)
+        self._pos2(pos2, pos1)
+        check(self._lib.q2gate_diag(self._p, ptr(g), pos2, pos1, self.qubits_number))
+
+    def apply_q2_gate_diag_conj(self, gate, pos2, pos1):
+        self.apply_q2_gate_diag(self._host(gate).conj(), pos2, pos1)
+
+    def get_q1_density(self, pos) -> np.ndarray:
+        d = np.zeros(4, self.dtype)
+        check(self._lib.get_q1density(self._p, ptr(d), pos, self.qubits_number))
+        return d
+
+    def get_q2_density(self, pos2, pos1) -> np.ndarray:
+        d = np.zeros(16, self.dtype)
+        check(self._lib.get_q2density(self._p, ptr(d), pos2, pos1, self.qubits_number))
+        return d
+
+
+def data_transfer(src: QuantizedTensor, dst: QuantizedTensor):
+    """quantized_tensor.rs:169-176."""
+    if src.qubits_number != dst.qubits_number:
+        raise PanicException("fwd and bwd have different lengths.")
+    src._lib.copy(src._p, dst._p, src.qubits_number)
+
+
+def _grad(fn, fwd, bwd, width, *pos):
+    if fwd.qubits_number != bwd.qubits_number:
+        raise PanicException("fwd and bwd have different lengths.")
+    g = np.zeros(width, fwd.dtype)
+    check(getattr(fwd._lib, fn)(fwd._p, bwd._p, ptr(g), *pos, fwd.qubits_number))
+    return g
+
+
+def get_q1_grad(fwd, bwd, pos):
+    """quantized_tensor.rs:178-189 (here the C error is checked; the reference ignores it)."""
+    return _grad("q1grad", fwd, bwd, 4, pos)
+
+
+def get_q2_grad(fwd, bwd, pos2, pos1):
+    """quantized_tensor.rs:191-205."""
+    return _grad("q2grad", fwd, bwd, 16, pos2, pos1)
+
+
+def get_q2_grad_diag(fwd, bwd, pos2, pos1):
+    """quantized_tensor.rs:207-221."""
+    return _grad("q2grad_diag", fwd, bwd, 4, pos2, pos1)

@@ -1,0 +1,120 @@
+/*
+ * qdc/circuit.h — native circuit interpreter over the HIP hot path.
+ *
+ * The reference implements this layer in Rust: `QuantizedTensor` (src/quantized_tensor.rs:
+ * 54-238) and the PyO3 class `Circuit` (src/circuit.rs:86-430).  Rust is not available on
+ * this platform, so the same semantics are provided by a C++ runtime behind this C ABI;
+ * the Python class `quantum_differentiable_circuit.Circuit` is a thin ctypes shim over it
+ * (see INTEGRATION.md for the equivalent Rust/cgo/ctypes bindings).
+ *
+ * Semantics follow circuit.rs exactly (instruction list, FIFO gate consumption, densities
+ * in instruction order, the O(1)-memory reverse sweep, zero gradients for variable gates
+ * met before any density cotangent, the panic messages).  What differs is only HOW it is
+ * executed: the reverse sweep is fused (uncompute + gradient + cotangent pull-back in one
+ * HBM pass), density cotangents are injected without a temporary state, and all gradients
+ * and densities stay on the device until one copy at the end of the call.
+ *
+ * Gates are passed flattened: `gates` = concatenation of every gate buffer, `lens[i]` = the
+ * number of complex entries of gate i.  Error convention as in primitives.h.
+ */
+#ifndef QDC_CIRCUIT_H
+#define QDC_CIRCUIT_H
+
+#include <stddef.h>
+
+#include "qdc/primitives.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Instruction kinds, in the order of `enum Instruction` (src/circuit.rs:53-68). */
+enum qdc_kind {
+  QDC_CONST_Q2 = 0,
+  QDC_VAR_Q2 = 1,
+  QDC_CONST_Q2_NONU = 2,
+  QDC_VAR_Q2_NONU = 3,
+  QDC_CONST_Q2_DIAG = 4,
+  QDC_VAR_Q2_DIAG = 5,
+  QDC_CONST_Q1 = 6,
+  QDC_CONST_Q1_NONU = 7,
+  QDC_VAR_Q1 = 8,
+  QDC_VAR_Q1_NONU = 9,
+  QDC_Q2_DENSITY = 10,
+  QDC_Q1_DENSITY = 11,
+  QDC_DIFF_Q2_DENSITY = 12,
+  QDC_DIFF_Q1_DENSITY = 13
+};
+
+/* Execution modes of qdc_circuit_execute: Circuit::run (circuit.rs:164-212) returns every
+ * density; Circuit::forward (circuit.rs:214-264) only the Diff* ones. */
+enum qdc_mode { QDC_MODE_RUN = 0, QDC_MODE_FORWARD = 1 };
+
+typedef struct qdc_circuit qdc_circuit;
+
+/* Circuit::new (circuit.rs:95-103): initial state |0...0>, on the current HIP device. */
+const char* qdc_circuit_new(qdc_circuit** out, size_t qubits_number);
+void qdc_circuit_free(qdc_circuit* c);
+size_t qdc_circuit_qubits(const qdc_circuit* c);
+
+/* Circuit::set_state_from_vector (circuit.rs:104-106 → quantized_tensor.rs:76-80). */
+const char* qdc_circuit_set_state_from_vector(qdc_circuit* c, const qdc_complex* vec,
+                                              size_t len);
+
+/* Circuit::add_* / get_*_dens_op* (circuit.rs:108-162).  For one-qubit kinds pass the
+ * position as `pos2` (pos1 is ignored). */
+const char* qdc_circuit_push(qdc_circuit* c, int kind, size_t pos2, size_t pos1);
+size_t qdc_circuit_len(const qdc_circuit* c);
+
+/* Number of complex values written to `densities` by qdc_circuit_execute(mode): 4 per
+ * one-qubit and 16 per two-qubit density, in instruction order. */
+size_t qdc_circuit_output_size(const qdc_circuit* c, int mode);
+/* Number of complex values written to `grads` by qdc_circuit_backward: 4 / 16 / 4 per
+ * Q1 / Q2 / Q2Diag variable gate, in forward order. */
+size_t qdc_circuit_grad_size(const qdc_circuit* c);
+
+/* Circuit::run / Circuit::forward. */
+const char* qdc_circuit_execute(qdc_circuit* c, int mode, const qdc_complex* const_gates,
+                                const size_t* const_lens, size_t n_const,
+                                const qdc_complex* var_gates, const size_t* var_lens,
+                                size_t n_var, qdc_complex* densities);
+
+/* Circuit::backward (circuit.rs:266-429).  `dens_grads` are the (already conjugated,
+ * circuit.py:193) cotangents of the Diff* densities, 4 or 16 entries each, forward order. */
+const char* qdc_circuit_backward(qdc_circuit* c, const qdc_complex* dens_grads,
+                                 const size_t* dens_lens, size_t n_dens,
+                                 const qdc_complex* const_gates, const size_t* const_lens,
+                                 size_t n_const, const qdc_complex* var_gates,
+                                 const size_t* var_lens, size_t n_var, qdc_complex* grads);
+
+/* Copies of the device states, for tests and debugging (QuantizedTensor::get_cpu_state_copy,
+ * quantized_tensor.rs:91-99).  which: 0 = current (fwd) state, 1 = initial state,
+ * 2 = backward state (after a backward call). */
+const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex* host, size_t len);
+
+/* Wait for all work queued by this circuit. */
+const char* qdc_circuit_sync(qdc_circuit* c);
+
+/* ---- measurement ------------------------------------------------------------------- */
+typedef struct qdc_kernel_stat {
+  char name[32];
+  size_t launches;
+  double total_ms;    /* sum of HIP-event durations of this kernel's launches */
+  double algo_bytes;  /* sum of algorithmic HBM bytes (SURVEY.md §8 d) */
+} qdc_kernel_stat;
+
+/* Bracket every launch of this circuit's stream with HIP events (on = 1) or stop (0);
+ * enabling clears previously collected records. */
+const char* qdc_circuit_profile(qdc_circuit* c, int on);
+/* Synchronise and aggregate the records per kernel name; returns the number of kernels
+ * (writes at most `cap` entries). */
+size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out, size_t cap);
+
+/* Library build information: "f32"/"f64", offload arch. */
+const char* qdc_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QDC_CIRCUIT_H */

