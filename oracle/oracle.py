@@ -433,7 +433,7 @@ def autodiff_circuit(n, layers, seed):
     ins += [(Q1_DENSITY, (i,)) for i in range(n)]
     ins += [(Q2_DENSITY, (i + 1, i)) for i in range(0, n - 1, 2)]
 
-    half = (n - 1) // 2
+    half = len(range(0, n - 1, 2))  # == int((n - 1) / 2) of test_autodiff.py for odd n
     nodd = len(range(1, n - 1, 2))
     const, var, pert = [], [], []
     for _ in range(layers):
