@@ -43,8 +43,9 @@ def parse():
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--seed", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-layers", type=int, default=1,
-                    help="layers of the CPU baseline sample (full n)")
+    ap.add_argument("--cpu-gates", type=int, default=12,
+                    help="gates of the CPU baseline sample (the workload's first gates, full n)")
+    ap.add_argument("--cpu-densities", type=int, default=4)
     ap.add_argument("--cpu-qubits", type=int, default=None)
     ap.add_argument("--pmc", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--micro", action="store_true", help="per-kernel bandwidth sweep")
@@ -112,28 +113,31 @@ def select_device(local):
         raise RuntimeError(f"hipSetDevice({local}) failed: {err}")
 
 
-def cpu_baseline(args, n, layers):
+def cpu_baseline(args, n):
     """Time the oracle's C/OpenMP restatement of the reference algorithm (unfused uncompute /
     grad / pull-back and allocate-conj-gate-add density injection, circuit.rs:266-429) on a
-    bounded sample of the same workload."""
+    bounded sample of the same workload: its first `cpu_gates` gates and `cpu_densities`
+    DiffQ1Density outputs, at full n."""
     from oracle import oracle as O
     from oracle.cref import CRefOps
     ops = CRefOps(args.precision)
-    ins, var = O.layered_circuit(n, layers, args.seed)
+    ins, var = O.layered_circuit(n, args.layers, args.seed)
+    gates = [(k, p) for k, p in ins if k < 10][:args.cpu_gates]
+    dens_ins = [(k, p) for k, p in ins if k >= 10][:args.cpu_densities]
     dt = ops.state_dtype
     o = O.OracleCircuit(n, dt, ops=ops)
-    for kind, pos in ins:
+    for kind, pos in gates + dens_ins:
         o.add(kind, *pos)
+    var = var[:len(gates)]
     t0 = time.perf_counter()
     dens = o.forward([], var)
     o.backward(sigma_z_cotangents(len(dens), dt), [], var)
     dt_s = time.perf_counter() - t0
-    gates = sum(1 for k, _ in ins if k < 10)
-    return {"value": gates / dt_s, "unit": "gate-applications/s (fwd+bwd)",
+    return {"value": len(gates) / dt_s, "unit": "gate-applications/s (fwd+bwd)",
             "cores": ops.threads(), "kind": "port",
-            "sample": f"{layers} layer(s) of the same circuit at n={n} {args.precision}: "
-                      f"{gates} gates fwd+bwd + {len(dens)} densities in {dt_s:.1f} s "
-                      f"(oracle/cpu_ref.c, OpenMP)"}
+            "sample": f"first {len(gates)} gates + {len(dens)} DiffQ1Density of the same "
+                      f"circuit at n={n} {args.precision}, fwd+bwd in {dt_s:.1f} s "
+                      f"(oracle/cpu_ref.c, OpenMP, reference algorithm unfused)"}
 
 
 def micro(args):
@@ -252,7 +256,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.cpu_qubits or n, args.cpu_layers)
+        cpu = cpu_baseline(args, args.cpu_qubits or n)
 
     if rank == 0:
         state_gib = (1 << n) * (8 if args.precision == "f32" else 16) / 2**30
