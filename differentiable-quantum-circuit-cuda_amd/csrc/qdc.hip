@@ -12,18 +12,11 @@ struct qdc_circuit {
 
 #define QDC_API extern "C" __attribute__((visibility("default")))
 
+static const char* new_circuit(qdc_circuit** out, size_t n, int world, int rank0, int nlocal,
+                               ncclComm_t comm);
+
 QDC_API const char* qdc_circuit_new(qdc_circuit** out, size_t qubits_number) {
-  *out = nullptr;
-  QDC_TRY(qdc::check_n(qubits_number));
-  qdc_circuit* c = new qdc_circuit();
-  const char* e = c->impl.init((uint32_t)qubits_number);
-  if (e) {
-    c->impl.destroy();
-    delete c;
-    return e;
-  }
-  *out = c;
-  return nullptr;
+  return new_circuit(out, qubits_number, 1, 0, 1, nullptr);
 }
 
 QDC_API void qdc_circuit_free(qdc_circuit* c) {
@@ -36,13 +29,17 @@ QDC_API size_t qdc_circuit_qubits(const qdc_circuit* c) { return c->impl.n; }
 
 QDC_API const char* qdc_circuit_set_state_from_vector(qdc_circuit* c, const qdc_complex* vec,
                                                       size_t len) {
-  // QuantizedTensor::set_from_host + get_qubits_number (quantized_tensor.rs:44-52, 76-80)
+  // QuantizedTensor::set_from_host + get_qubits_number (quantized_tensor.rs:44-52, 76-80);
+  // a sharded circuit takes its slices of the full vector (the initial layout is identity)
+  qdc::Circuit& k = c->impl;
   if (len == 0 || (len & (len - 1)) != 0) return qdc::fail("State size is not a power of 2.");
-  if (len != ((size_t)1 << c->impl.n))
+  if (len != ((size_t)1 << k.n))
     return qdc::fail("Size of the given state does not match the size of the tensor.");
-  QDC_HIP(hipMemcpyAsync(c->impl.initial, vec, len * sizeof(qdc_complex), hipMemcpyHostToDevice,
-                         c->impl.ctx.stream));
-  QDC_HIP(hipStreamSynchronize(c->impl.ctx.stream));
+  const size_t shard = (size_t)1 << k.nl;
+  for (size_t s = 0; s < k.sh.size(); ++s)
+    QDC_HIP(hipMemcpyAsync(k.sh[s].initial, vec + (size_t)(k.ex.rank0 + s) * shard,
+                           shard * sizeof(qdc_complex), hipMemcpyHostToDevice, k.ctx.stream));
+  QDC_HIP(hipStreamSynchronize(k.ctx.stream));
   return nullptr;
 }
 
@@ -77,16 +74,125 @@ QDC_API const char* qdc_circuit_backward(qdc_circuit* c, const qdc_complex* dg, 
   return c->impl.backward(df, cf, vf, grads);
 }
 
-QDC_API const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex* host,
-                                          size_t len) {
+QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
+                                          qdc_complex* host, size_t len) {
   qdc::Circuit& k = c->impl;
-  if (len != ((size_t)1 << k.n)) return qdc::fail("state length mismatch");
-  const qdc::cx* src = which == 0 ? k.state : which == 1 ? k.initial : k.bwd;
+  if (shard < 0 || (size_t)shard >= k.sh.size()) return qdc::fail("no local shard %d", shard);
+  if (len != ((size_t)1 << k.nl)) return qdc::fail("shard length mismatch");
+  const qdc::Shard& s = k.sh[shard];
+  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
   if (!src) return qdc::fail("state %d is not allocated", which);
   QDC_HIP(hipMemcpyAsync(host, src, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
                          k.ctx.stream));
   QDC_HIP(hipStreamSynchronize(k.ctx.stream));
   return nullptr;
+}
+
+// Unsharded circuits only (a sharded state is assembled from qdc_circuit_get_shard + layout).
+QDC_API const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex* host,
+                                          size_t len) {
+  qdc::Circuit& k = c->impl;
+  if (k.g != 0) return qdc::fail("sharded state: use qdc_circuit_get_shard and qdc_circuit_layout");
+  if (len != ((size_t)1 << k.n)) return qdc::fail("state length mismatch");
+  return qdc_circuit_get_shard(c, which, 0, host, len);
+}
+
+QDC_API const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world,
+                                       int* rank, int* local_shards) {
+  const qdc::Circuit& k = c->impl;
+  if (phys)
+    for (uint32_t q = 0; q < k.n; ++q) phys[q] = k.layout.phys[q];
+  if (world) *world = k.ex.world;
+  if (rank) *rank = k.ex.rank0;
+  if (local_shards) *local_shards = (int)k.sh.size();
+  return nullptr;
+}
+
+// ---- communicator + sharded constructors ---------------------------------------------------
+struct qdc_comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+};
+
+QDC_API const char* qdc_comm_unique_id(unsigned char id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  ncclUniqueId u;
+  QDC_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof(u));
+  return nullptr;
+}
+
+QDC_API const char* qdc_comm_init(qdc_comm** out, int rank, int world,
+                                  const unsigned char id[128]) {
+  *out = nullptr;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  qdc_comm* c = new qdc_comm();
+  c->rank = rank;
+  c->world = world;
+  const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return qdc::fail("RCCL ERROR: ncclCommInitRank failed with %s.", ncclGetErrorString(r));
+  }
+  *out = c;
+  return nullptr;
+}
+
+QDC_API void qdc_comm_free(qdc_comm* c) {
+  if (!c) return;
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+static const char* new_circuit(qdc_circuit** out, size_t n, int world, int rank0, int nlocal,
+                               ncclComm_t comm) {
+  *out = nullptr;
+  QDC_TRY(qdc::check_n(n));
+  qdc_circuit* c = new qdc_circuit();
+  const char* e = c->impl.init((uint32_t)n, world, rank0, nlocal, comm);
+  if (e) {
+    c->impl.destroy();
+    delete c;
+    return e;
+  }
+  *out = c;
+  return nullptr;
+}
+
+QDC_API const char* qdc_circuit_new_sharded(qdc_circuit** out, size_t n, qdc_comm* comm) {
+  if (!comm) return qdc::fail("no communicator");
+  return new_circuit(out, n, comm->world, comm->rank, 1, comm->world > 1 ? comm->comm : nullptr);
+}
+
+QDC_API const char* qdc_circuit_new_local_shards(qdc_circuit** out, size_t n, int shards) {
+  if (shards < 1) return qdc::fail("shards must be >= 1");
+  return new_circuit(out, n, shards, 0, shards, nullptr);
+}
+
+// ---- planner -----------------------------------------------------------------------------
+QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned* pos2,
+                        const unsigned* pos1, size_t count, int mode, const unsigned* start_phys,
+                        qdc_plan_op* out, size_t cap, unsigned* end_phys) {
+  const uint32_t g = qdc::log2_exact(world);
+  if (g == UINT32_MAX || n < 2 * (size_t)g + 3 || n > 64) return 0;
+  std::vector<qdc::PlanIn> all(count);
+  for (size_t i = 0; i < count; ++i) all[i] = {kinds[i], pos2[i], pos1[i]};
+  std::vector<qdc::PlanIn> ops;
+  std::vector<int> index;
+  qdc::active_ops(all, mode, ops, index);
+  qdc::QubitMap m;
+  m.identity((uint32_t)n, g);
+  if (start_phys) {
+    for (uint32_t q = 0; q < n; ++q) m.phys[q] = start_phys[q];
+    for (uint32_t q = 0; q < n; ++q) m.logi[m.phys[q]] = q;
+  }
+  std::vector<qdc_plan_op> plan;
+  qdc::plan_pass(ops, index, m, plan);
+  for (size_t i = 0; i < plan.size() && i < cap; ++i) out[i] = plan[i];
+  if (end_phys)
+    for (uint32_t q = 0; q < n; ++q) end_phys[q] = m.phys[q];
+  return plan.size();
 }
 
 QDC_API const char* qdc_circuit_sync(qdc_circuit* c) {

@@ -12,8 +12,11 @@
 #include <cstring>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "qdc/circuit.h"
 #include "qdc_device.hpp"
+#include "qdc_shard.hpp"
 
 namespace qdc {
 
@@ -92,50 +95,141 @@ inline const char* check_density_pos(const Instr& in, uint32_t n) {
   return nullptr;
 }
 
-struct Circuit {
-  uint32_t n = 0;
-  Ctx ctx;
+#define QDC_NCCL(call)                                                                   \
+  do {                                                                                   \
+    ncclResult_t qdc_r_ = (call);                                                        \
+    if (qdc_r_ != ncclSuccess)                                                           \
+      return ::qdc::fail("RCCL ERROR: call of a function \"%s\" in line %d of file %s "  \
+                         "failed with %s.",                                              \
+                         #call, __LINE__, __FILE__, ncclGetErrorString(qdc_r_));          \
+  } while (0)
+
+// The shard exchange.  RCCL: one shard per process (one rank per GPU, xGMI); loopback: every
+// shard in this process on the current GPU, exchanged with device-to-device copies.
+struct Exchange {
+  int world = 1;   // total shards
+  int rank0 = 0;   // global index of this process's first shard
+  int nlocal = 1;  // shards held by this process
+  ncclComm_t comm = nullptr;
+
+  // Block j of send[s] (chunk amplitudes) goes to shard j and lands as block s of recv[j].
+  const char* alltoall(Ctx& c, std::vector<cx*>& send, std::vector<cx*>& recv, size_t chunk) {
+    if (world == 1) return nullptr;
+    const double bytes = (double)chunk * sizeof(cx) * (world - 1) * nlocal;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c.prof.on) {
+      a = c.prof.get();
+      b = c.prof.get();
+      if (a) (void)hipEventRecord(a, c.stream);
+    }
+    if (comm) {
+      QDC_NCCL(ncclAllToAll(send[0], recv[0], chunk * 2, sizeof(real) == 4 ? ncclFloat : ncclDouble,
+                            comm, c.stream));
+    } else {
+      for (int s = 0; s < nlocal; ++s)
+        for (int d = 0; d < nlocal; ++d)
+          QDC_HIP(hipMemcpyAsync(recv[d] + (size_t)s * chunk, send[s] + (size_t)d * chunk,
+                                 chunk * sizeof(cx), hipMemcpyDeviceToDevice, c.stream));
+    }
+    if (c.prof.on && a && b) {
+      (void)hipEventRecord(b, c.stream);
+      c.prof.recs.push_back({"alltoall", bytes, a, b});  // link bytes, not HBM bytes
+    }
+    return nullptr;
+  }
+  // in-place sum over all shards of `count` complex values
+  const char* allreduce(Ctx& c, std::vector<cx*>& bufs, size_t count) {
+    if (world == 1 || count == 0) return nullptr;
+    if (comm) {
+      QDC_NCCL(ncclAllReduce(bufs[0], bufs[0], count * 2, sizeof(real) == 4 ? ncclFloat : ncclDouble,
+                             ncclSum, comm, c.stream));
+      return nullptr;
+    }
+    for (int s = 1; s < nlocal; ++s) QDC_TRY(elementwise_count<2>(c, bufs[s], bufs[0], count));
+    for (int s = 1; s < nlocal; ++s)
+      QDC_HIP(hipMemcpyAsync(bufs[s], bufs[0], count * sizeof(cx), hipMemcpyDeviceToDevice,
+                             c.stream));
+    return nullptr;
+  }
+};
+
+struct Shard {
   cx* initial = nullptr;
   cx* state = nullptr;
   cx* bwd = nullptr;
-  cx* dens_dev = nullptr;
-  size_t dens_cap = 0;
-  cx* grads_dev = nullptr;
-  size_t grads_cap = 0;
+  cx* scratch = nullptr;  // all-to-all staging (allocated when world > 1)
+  cx* dens = nullptr;
+  cx* grads = nullptr;
+};
+
+struct Circuit {
+  uint32_t n = 0;   // logical qubits
+  uint32_t g = 0;   // rank bits
+  uint32_t nl = 0;  // local qubits of a shard
+  Ctx ctx;
+  Exchange ex;
+  std::vector<Shard> sh;
+  QubitMap layout;  // physical layout of every shard's `state` (identity until a remap)
+  size_t dens_cap = 0, grads_cap = 0;
   cx* host_out = nullptr;  // pinned
   size_t host_cap = 0;
   std::vector<Instr> ins;
 
-  const char* init(uint32_t qubits) {
+  // world = total shards (power of two), nlocal = shards in this process
+  const char* init(uint32_t qubits, int world = 1, int rank0 = 0, int nlocal = 1,
+                   ncclComm_t comm = nullptr) {
     n = qubits;
+    const uint32_t gg = log2_exact((size_t)world);
+    if (gg == UINT32_MAX || gg > 8) return fail("the number of shards must be a power of two <= 256");
+    g = gg;
+    if (g > 0 && n < 2 * g + 3)
+      return fail("%u qubits are too few to shard over %d ranks (need >= %u)", n, world, 2 * g + 3);
+    nl = n - g;
+    ex.world = world;
+    ex.rank0 = rank0;
+    ex.nlocal = nlocal;
+    ex.comm = comm;
+    layout.identity(n, g);
     int dev = 0;
     QDC_HIP(hipGetDevice(&dev));
     QDC_TRY(ctx.init(dev));
-    const size_t bytes = ((size_t)1 << n) * sizeof(cx);
-    QDC_HIP(hipMalloc(&initial, bytes));
-    QDC_HIP(hipMalloc(&state, bytes));
-    // QuantizedTensor::new_standard + clone (circuit.rs:96-102)
-    QDC_TRY(set_standard(ctx, initial, n));
-    QDC_TRY(elementwise<0>(ctx, initial, state, n));
+    const size_t bytes = ((size_t)1 << nl) * sizeof(cx);
+    sh.resize(nlocal);
+    for (int s = 0; s < nlocal; ++s) {
+      QDC_HIP(hipMalloc(&sh[s].initial, bytes));
+      QDC_HIP(hipMalloc(&sh[s].state, bytes));
+      if (g > 0) QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
+      // QuantizedTensor::new_standard + clone (circuit.rs:96-102): |0..0> lives on shard 0
+      if (rank0 + s == 0)
+        QDC_TRY(set_standard(ctx, sh[s].initial, nl));
+      else
+        QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, ctx.stream));
+      QDC_TRY(elementwise<0>(ctx, sh[s].initial, sh[s].state, nl));
+    }
     QDC_HIP(hipStreamSynchronize(ctx.stream));
     return nullptr;
   }
   void destroy() {
     if (ctx.stream) (void)hipStreamSynchronize(ctx.stream);
-    for (cx* p : {initial, state, bwd, dens_dev, grads_dev})
-      if (p) (void)hipFree(p);
+    for (auto& s : sh)
+      for (cx* p : {s.initial, s.state, s.bwd, s.scratch, s.dens, s.grads})
+        if (p) (void)hipFree(p);
+    sh.clear();
     if (host_out) (void)hipHostFree(host_out);
+    host_out = nullptr;
     ctx.destroy();
   }
 
-  const char* ensure_dev(cx*& p, size_t& cap, size_t count) {
+  const char* ensure_out(bool dens, size_t count) {
+    size_t& cap = dens ? dens_cap : grads_cap;
     if (count <= cap) return nullptr;
-    if (p) {
-      QDC_HIP(hipStreamSynchronize(ctx.stream));
-      QDC_HIP(hipFree(p));
+    QDC_HIP(hipStreamSynchronize(ctx.stream));
+    for (auto& s : sh) {
+      cx*& p = dens ? s.dens : s.grads;
+      if (p) QDC_HIP(hipFree(p));
+      p = nullptr;
+      QDC_HIP(hipMalloc(&p, sizeof(cx) * count));
     }
-    p = nullptr;
-    QDC_HIP(hipMalloc(&p, sizeof(cx) * count));
     cap = count;
     return nullptr;
   }
@@ -176,9 +270,7 @@ struct Circuit {
     return c;
   }
 
-  // --- forward (Circuit::run / Circuit::forward) --------------------------------------
-  // Validation reproduces the reference's panic order: per instruction, pop then the
-  // apply-time assertions; leftovers at the end (circuit.rs:170-211, 221-263).
+  // --- validation: the reference's panic order (circuit.rs:170-211, 221-263, 274-428) --------
   const char* validate_forward(const Flat& cg, const Flat& vg, std::vector<size_t>& gidx) const {
     if (ins.empty()) return fail("The circuit is empty.");
     size_t ci = 0, vi = 0;
@@ -209,70 +301,6 @@ struct Circuit {
     return nullptr;
   }
 
-  const char* apply_forward(const Instr& in, const qdc_complex* g, cx* s) {
-    if (is_q1_gate(in.kind)) return apply_dense<2>(ctx, s, to_mat<2>(g), in.a, in.a, n, "apply_q1");
-    if (is_q2_dense(in.kind))
-      return apply_dense<4>(ctx, s, to_mat<4>(g), in.a, in.b, n, "apply_q2");
-    return apply_diag(ctx, s, to_diag(g), in.a, in.b, n, "apply_q2_diag");
-  }
-
-  const char* execute(int mode, const Flat& cg, const Flat& vg, qdc_complex* out) {
-    std::vector<size_t> gidx;
-    QDC_TRY(validate_forward(cg, vg, gidx));
-    const size_t nout = output_count(mode);
-    QDC_TRY(ensure_dev(dens_dev, dens_cap, std::max<size_t>(nout, 1) * RED));
-    QDC_TRY(elementwise<0>(ctx, initial, state, n));  // data_transfer (quantized_tensor.rs:169-176)
-    uint32_t o = 0;
-    for (size_t k = 0; k < ins.size(); ++k) {
-      const Instr& in = ins[k];
-      if (is_const(in.kind)) {
-        QDC_TRY(apply_forward(in, cg.at(gidx[k]), state));
-      } else if (is_var(in.kind)) {
-        QDC_TRY(apply_forward(in, vg.at(gidx[k]), state));
-      } else if (is_diff_density(in.kind) || mode == QDC_MODE_RUN) {
-        if (is_q1_density(in.kind))
-          QDC_TRY(density<2>(ctx, state, in.a, in.a, n, dens_dev, o++, 0));
-        else
-          QDC_TRY(density<4>(ctx, state, in.a, in.b, n, dens_dev, o++, 0));
-      }
-    }
-    QDC_TRY(ctx.flush());
-    return collect(dens_dev, nout, out, [&](size_t j) {
-      size_t c = 0;
-      for (auto& in : ins)
-        if (is_diff_density(in.kind) || (mode == QDC_MODE_RUN && is_density(in.kind))) {
-          if (c == j) return is_q1_density(in.kind) ? 4 : 16;
-          ++c;
-        }
-      return 0;
-    });
-  }
-
-  template <class F>
-  const char* collect(const cx* dev, size_t count, qdc_complex* out, F width_of) {
-    if (count == 0) {
-      QDC_HIP(hipStreamSynchronize(ctx.stream));
-      return nullptr;
-    }
-    QDC_TRY(ensure_host(count * RED));
-    QDC_HIP(hipMemcpyAsync(host_out, dev, sizeof(cx) * count * RED, hipMemcpyDeviceToHost,
-                           ctx.stream));
-    QDC_HIP(hipStreamSynchronize(ctx.stream));
-    // widths are computed once, in order
-    size_t w = 0;
-    std::vector<int> widths(count);
-    for (size_t j = 0; j < count; ++j) widths[j] = width_of(j);
-    for (size_t j = 0; j < count; ++j) {
-      for (int k = 0; k < widths[j]; ++k) {
-        out[w + k].re = host_out[j * RED + k].x;
-        out[w + k].im = host_out[j * RED + k].y;
-      }
-      w += widths[j];
-    }
-    return nullptr;
-  }
-
-  // --- backward (Circuit::backward, circuit.rs:266-429) --------------------------------
   const char* validate_backward(const Flat& dg, const Flat& cg, const Flat& vg,
                                 std::vector<size_t>& gidx) const {
     if (ins.empty()) return fail("The circuit is empty.");
@@ -308,70 +336,214 @@ struct Circuit {
     return nullptr;
   }
 
+  // --- remap: one all-to-all per state (see qdc_shard.hpp) --------------------------------
+  const char* remap(const qdc_plan_op& r, bool with_bwd) {
+    const uint32_t low = nl - g;              // amplitude bits of one all-to-all block
+    const size_t chunk = (size_t)1 << low;    // amplitudes per block
+    for (int which = 0; which < (with_bwd ? 2 : 1); ++which) {
+      std::vector<cx*> send(sh.size()), recv(sh.size());
+      for (size_t s = 0; s < sh.size(); ++s) {
+        cx*& buf = which == 0 ? sh[s].state : sh[s].bwd;
+        if (r.pack) {
+          QDC_TRY(pack(ctx, buf, sh[s].scratch, r.victims, g, nl));
+          send[s] = sh[s].scratch;
+          recv[s] = buf;
+        } else {
+          send[s] = buf;
+          recv[s] = sh[s].scratch;
+        }
+      }
+      QDC_TRY(ex.alltoall(ctx, send, recv, chunk));
+      if (!r.pack)
+        for (size_t s = 0; s < sh.size(); ++s)
+          std::swap(which == 0 ? sh[s].state : sh[s].bwd, sh[s].scratch);
+    }
+    layout.apply(r.victims);
+    return nullptr;
+  }
+
+  std::vector<qdc_plan_op> plan(int mode) const {
+    std::vector<PlanIn> ops;
+    std::vector<int> index;
+    active_ops(ins, mode, ops, index);
+    QubitMap m = layout;
+    std::vector<qdc_plan_op> out;
+    plan_pass(ops, index, m, out);
+    return out;
+  }
+
+  // --- forward (Circuit::run / Circuit::forward) --------------------------------------------
+  const char* apply_gate(const Instr& in, const qdc_complex* g4, cx* s, uint32_t p2, uint32_t p1,
+                         bool uncompute) {
+    if (is_diag(in.kind)) {
+      const diag4 d = to_diag(g4);
+      return apply_diag(ctx, s, uncompute ? conj_diag(d) : d, p2, p1, nl,
+                        uncompute ? "uncompute_q2_diag" : "apply_q2_diag");
+    }
+    if (is_q1_gate(in.kind)) {
+      const mat<2> u = to_mat<2>(g4);
+      mat<2> a = u;
+      if (uncompute) {
+        if (is_nonu(in.kind))
+          QDC_TRY(inverse<2>(u, a));
+        else
+          a = conj_transpose<2>(u);
+      }
+      return apply_dense<2>(ctx, s, a, p2, p2, nl, uncompute ? "uncompute_q1" : "apply_q1");
+    }
+    const mat<4> u = to_mat<4>(g4);
+    mat<4> a = u;
+    if (uncompute) {
+      if (is_nonu(in.kind))
+        QDC_TRY(inverse<4>(u, a));
+      else
+        a = conj_transpose<4>(u);
+    }
+    return apply_dense<4>(ctx, s, a, p2, p1, nl, uncompute ? "uncompute_q2" : "apply_q2");
+  }
+
+  const char* execute(int mode, const Flat& cg, const Flat& vg, qdc_complex* out) {
+    std::vector<size_t> gidx;
+    QDC_TRY(validate_forward(cg, vg, gidx));
+    const size_t nout = output_count(mode);
+    QDC_TRY(ensure_out(true, std::max<size_t>(nout, 1) * RED));
+    // every pass starts from `initial`, which is always in the identity layout
+    layout.identity(n, g);
+    for (auto& s : sh) QDC_TRY(elementwise<0>(ctx, s.initial, s.state, nl));
+    std::vector<uint32_t> out_idx(ins.size(), 0);
+    {
+      uint32_t o = 0;
+      for (size_t k = 0; k < ins.size(); ++k)
+        if (is_diff_density(ins[k].kind) || (mode == QDC_MODE_RUN && is_density(ins[k].kind)))
+          out_idx[k] = o++;
+    }
+    for (const qdc_plan_op& op : plan(mode)) {
+      if (op.type == QDC_PLAN_REMAP) {
+        QDC_TRY(remap(op, false));
+        continue;
+      }
+      const Instr& in = ins[op.instr];
+      for (auto& s : sh) {
+        if (is_const(in.kind) || is_var(in.kind)) {
+          const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
+          QDC_TRY(apply_gate(in, g4, s.state, op.pos2, op.pos1, false));
+        } else if (is_q1_density(in.kind)) {
+          QDC_TRY(density<2>(ctx, s.state, op.pos2, op.pos2, nl, s.dens, out_idx[op.instr], 0));
+        } else {
+          QDC_TRY(density<4>(ctx, s.state, op.pos2, op.pos1, nl, s.dens, out_idx[op.instr], 0));
+        }
+      }
+    }
+    QDC_TRY(ctx.flush());
+    std::vector<cx*> bufs;
+    for (auto& s : sh) bufs.push_back(s.dens);
+    QDC_TRY(ex.allreduce(ctx, bufs, nout * RED));
+    std::vector<int> widths;
+    for (auto& in : ins)
+      if (is_diff_density(in.kind) || (mode == QDC_MODE_RUN && is_density(in.kind)))
+        widths.push_back(is_q1_density(in.kind) ? 4 : 16);
+    return collect(sh[0].dens, widths, out);
+  }
+
+  const char* collect(const cx* dev, const std::vector<int>& widths, qdc_complex* out) {
+    const size_t count = widths.size();
+    if (count == 0) {
+      QDC_HIP(hipStreamSynchronize(ctx.stream));
+      return nullptr;
+    }
+    QDC_TRY(ensure_host(count * RED));
+    QDC_HIP(hipMemcpyAsync(host_out, dev, sizeof(cx) * count * RED, hipMemcpyDeviceToHost,
+                           ctx.stream));
+    QDC_HIP(hipStreamSynchronize(ctx.stream));
+    size_t w = 0;
+    for (size_t j = 0; j < count; ++j) {
+      for (int k = 0; k < widths[j]; ++k) {
+        out[w + k].re = host_out[j * RED + k].x;
+        out[w + k].im = host_out[j * RED + k].y;
+      }
+      w += widths[j];
+    }
+    return nullptr;
+  }
+
+  // --- backward (Circuit::backward, circuit.rs:266-429) --------------------------------------
   const char* backward(const Flat& dg, const Flat& cg, const Flat& vg, qdc_complex* out) {
     std::vector<size_t> gidx;
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
     const size_t nvar = n_var();
-    if (!bwd) QDC_HIP(hipMalloc(&bwd, ((size_t)1 << n) * sizeof(cx)));
-    QDC_TRY(ensure_dev(grads_dev, grads_cap, std::max<size_t>(nvar, 1) * RED));
+    for (auto& s : sh)
+      if (!s.bwd) QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
+    QDC_TRY(ensure_out(false, std::max<size_t>(nvar, 1) * RED));
     // variable gates met before the first cotangent keep zero gradients (circuit.rs:327-331)
-    QDC_HIP(hipMemsetAsync(grads_dev, 0, sizeof(cx) * std::max<size_t>(nvar, 1) * RED,
-                           ctx.stream));
-    cx* f = state;
+    for (auto& s : sh)
+      QDC_HIP(hipMemsetAsync(s.grads, 0, sizeof(cx) * std::max<size_t>(nvar, 1) * RED,
+                             ctx.stream));
+    std::vector<uint32_t> var_idx(ins.size(), 0);
+    {
+      uint32_t v = 0;
+      for (size_t k = 0; k < ins.size(); ++k)
+        if (is_var(ins[k].kind)) var_idx[k] = v++;
+    }
     bool have_bwd = false;
-    size_t var_no = nvar;  // forward index of the next variable gate met in reverse
-    for (size_t kk = ins.size(); kk-- > 0;) {
-      const Instr& in = ins[kk];
+    for (const qdc_plan_op& op : plan(QDC_PLAN_BACKWARD)) {
+      if (op.type == QDC_PLAN_REMAP) {
+        QDC_TRY(remap(op, have_bwd));
+        continue;
+      }
+      const Instr& in = ins[op.instr];
       if (is_const(in.kind) || is_var(in.kind)) {
         const bool var = is_var(in.kind);
-        if (var) --var_no;
-        const qdc_complex* g = var ? vg.at(gidx[kk]) : cg.at(gidx[kk]);
-        cx* gbase = (var && have_bwd) ? grads_dev : nullptr;
-        if (is_diag(in.kind)) {
-          const diag4 d = to_diag(g);
-          if (have_bwd)
-            QDC_TRY(reverse_diag(ctx, f, bwd, d, in.a, in.b, n, gbase, (uint32_t)var_no));
-          else
-            QDC_TRY(apply_diag(ctx, f, conj_diag(d), in.a, in.b, n, "uncompute_q2_diag"));
-        } else if (is_q1_gate(in.kind)) {
-          const mat<2> u = to_mat<2>(g);
-          mat<2> A;
-          if (is_nonu(in.kind))
-            QDC_TRY(inverse<2>(u, A));
-          else
-            A = conj_transpose<2>(u);
-          if (have_bwd)
-            QDC_TRY(reverse_dense<2>(ctx, f, bwd, A, transpose<2>(u), in.a, in.a, n, gbase,
-                                     (uint32_t)var_no));
-          else
-            QDC_TRY(apply_dense<2>(ctx, f, A, in.a, in.a, n, "uncompute_q1"));
-        } else {
-          const mat<4> u = to_mat<4>(g);
-          mat<4> A;
-          if (is_nonu(in.kind))
-            QDC_TRY(inverse<4>(u, A));
-          else
-            A = conj_transpose<4>(u);
-          if (have_bwd)
-            QDC_TRY(reverse_dense<4>(ctx, f, bwd, A, transpose<4>(u), in.a, in.b, n, gbase,
-                                     (uint32_t)var_no));
-          else
-            QDC_TRY(apply_dense<4>(ctx, f, A, in.a, in.b, n, "uncompute_q2"));
+        const qdc_complex* g4 = var ? vg.at(gidx[op.instr]) : cg.at(gidx[op.instr]);
+        for (auto& s : sh) {
+          if (!have_bwd) {
+            QDC_TRY(apply_gate(in, g4, s.state, op.pos2, op.pos1, true));
+            continue;
+          }
+          cx* gbase = var ? s.grads : nullptr;
+          const uint32_t dst = var_idx[op.instr];
+          if (is_diag(in.kind)) {
+            QDC_TRY(reverse_diag(ctx, s.state, s.bwd, to_diag(g4), op.pos2, op.pos1, nl, gbase, dst));
+          } else if (is_q1_gate(in.kind)) {
+            const mat<2> u = to_mat<2>(g4);
+            mat<2> A;
+            if (is_nonu(in.kind))
+              QDC_TRY(inverse<2>(u, A));
+            else
+              A = conj_transpose<2>(u);
+            QDC_TRY(reverse_dense<2>(ctx, s.state, s.bwd, A, transpose<2>(u), op.pos2, op.pos2, nl,
+                                     gbase, dst));
+          } else {
+            const mat<4> u = to_mat<4>(g4);
+            mat<4> A;
+            if (is_nonu(in.kind))
+              QDC_TRY(inverse<4>(u, A));
+            else
+              A = conj_transpose<4>(u);
+            QDC_TRY(reverse_dense<4>(ctx, s.state, s.bwd, A, transpose<4>(u), op.pos2, op.pos1, nl,
+                                     gbase, dst));
+          }
         }
-      } else if (is_diff_density(in.kind)) {
-        const qdc_complex* gd = dg.at(gidx[kk]);
-        if (is_q1_density(in.kind))
-          QDC_TRY(inject<2>(ctx, f, bwd, transpose<2>(to_mat<2>(gd)), in.a, in.a, n, !have_bwd));
-        else
-          QDC_TRY(inject<4>(ctx, f, bwd, transpose<4>(to_mat<4>(gd)), in.a, in.b, n, !have_bwd));
+      } else {  // Diff density: inject its cotangent
+        const qdc_complex* gd = dg.at(gidx[op.instr]);
+        for (auto& s : sh) {
+          if (is_q1_density(in.kind))
+            QDC_TRY(inject<2>(ctx, s.state, s.bwd, transpose<2>(to_mat<2>(gd)), op.pos2, op.pos2, nl,
+                              !have_bwd));
+          else
+            QDC_TRY(inject<4>(ctx, s.state, s.bwd, transpose<4>(to_mat<4>(gd)), op.pos2, op.pos1, nl,
+                              !have_bwd));
+        }
         have_bwd = true;
       }
     }
     QDC_TRY(ctx.flush());
+    std::vector<cx*> bufs;
+    for (auto& s : sh) bufs.push_back(s.grads);
+    QDC_TRY(ex.allreduce(ctx, bufs, nvar * RED));
     std::vector<int> widths;
     for (auto& in : ins)
       if (is_var(in.kind)) widths.push_back(gate_len(in.kind));
-    return collect(grads_dev, nvar, out, [&](size_t j) { return widths[j]; });
+    return collect(sh[0].grads, widths, out);
   }
 };
 

@@ -537,6 +537,28 @@ inline const char* elementwise(Ctx& c, const cx* src, cx* dst, uint32_t n) {
   return c.launch(names[OP], bytes, k_elementwise<OP>, grid, src, dst, amps, it);
 }
 
+// the same kernels over an arbitrary number of complex values (reduction buffers)
+template <int OP>
+inline const char* elementwise_count(Ctx& c, const cx* src, cx* dst, uint64_t count) {
+  const uint64_t nch = count / VEC > 0 ? count / VEC : 1;
+  const uint32_t it = per_thread(nch, c.grid_cap);
+  const uint32_t grid = (uint32_t)((nch + (uint64_t)BLOCK * it - 1) / ((uint64_t)BLOCK * it));
+  return c.launch("reduce_sum", 0.0, k_elementwise<OP>, grid, src, dst, count, it);
+}
+
+// remap pack of one shard of nl local qubits (victims: ascending amplitude positions >= 1)
+inline const char* pack(Ctx& c, const cx* src, cx* dst, const unsigned* victims, uint32_t g,
+                        uint32_t nl) {
+  packgeo pg{};
+  pg.nchunks = nchunks_of(nl);
+  pg.lowc = (nl - g) - LV;
+  pg.g = g;
+  for (uint32_t k = 0; k < g; ++k) pg.vc[k] = victims[k] - LV;
+  const uint32_t grid = (uint32_t)((pg.nchunks + BLOCK - 1) / BLOCK);
+  return c.launch("remap_pack", 2.0 * state_bytes(nl), k_pack, grid,
+                  reinterpret_cast<const chunk*>(src), reinterpret_cast<chunk*>(dst), pg);
+}
+
 inline const char* set_standard(Ctx& c, cx* s, uint32_t n) {
   return elementwise<3>(c, nullptr, s, n);
 }

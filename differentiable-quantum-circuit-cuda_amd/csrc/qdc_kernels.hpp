@@ -537,6 +537,30 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
 }
 
 // ---------------------------------------------------------------------------------------
+// Remap pack (qdc_shard.hpp): dst block j (victim bit pattern j) = the source chunks whose
+// victim bits equal j, in order.  dst[o] = src[expand(o)]: insert zeros at the victim chunk
+// bits (ascending) into the low part of o, then deposit the block index bits there.  One
+// chunk per thread; victims are high local bits, so every wave stays on a contiguous KiB.
+// ---------------------------------------------------------------------------------------
+struct packgeo {
+  uint64_t nchunks;
+  uint32_t lowc;   // chunk bits of one block
+  uint32_t g;      // victims
+  uint32_t vc[8];  // victim chunk bits, ascending
+};
+
+__global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
+                                                chunk* __restrict__ dst, packgeo pg) {
+  const uint64_t o = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (o >= pg.nchunks) return;
+  const uint64_t j = o >> pg.lowc;
+  uint64_t idx = o & ((1ull << pg.lowc) - 1ull);
+  for (uint32_t k = 0; k < pg.g; ++k) idx = insert_zero(idx, pg.vc[k]);
+  for (uint32_t k = 0; k < pg.g; ++k) idx |= ((j >> k) & 1ull) << pg.vc[k];
+  stc(dst + o, ldc(src + idx));
+}
+
+// ---------------------------------------------------------------------------------------
 // Elementwise state kernels (primitives.cu:176-187, 879-939).
 // op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>
 // ---------------------------------------------------------------------------------------

@@ -20,11 +20,12 @@ from typing import List, Sequence
 
 import numpy as np
 
-from ._native import (PanicException, KernelStat, check, default_precision, load, ptr,
-                      PRECISIONS)
+from ._native import (PanicException, KernelStat, PlanOp, check, default_precision, load,
+                      ptr, PRECISIONS)
 
 __all__ = ["Circuit", "Circuit32", "Circuit64", "QuantizedTensor", "PanicException",
-           "get_q1_grad", "get_q2_grad", "get_q2_grad_diag", "data_transfer", "circuit_class"]
+           "get_q1_grad", "get_q2_grad", "get_q2_grad_diag", "data_transfer", "circuit_class",
+           "plan", "unpermute"]
 
 # enum Instruction order (src/circuit.rs:53-68) == enum qdc_kind (include/qdc/circuit.h)
 (CONST_Q2, VAR_Q2, CONST_Q2_NONU, VAR_Q2_NONU, CONST_Q2_DIAG, VAR_Q2_DIAG, CONST_Q1,
@@ -59,11 +60,23 @@ def _flatten(arrays, dtype, what, msg):
 class _CircuitBase:
     _precision = "f32"
 
-    def __init__(self, qubits_number: int):
+    def __init__(self, qubits_number: int, comm=None, local_shards: int | None = None):
+        """`comm` (a `distributed.Communicator`) shards the state over its ranks, one GPU per
+        process; `local_shards=G` keeps G shards on this GPU (same data path, device copies
+        instead of RCCL).  Neither exists in the reference, which is single-GPU."""
         self._lib = load(self._precision)
         self._dtype = np.dtype(PRECISIONS[self._precision])
         h = C.c_void_p()
-        check(self._lib.qdc_circuit_new(C.byref(h), int(qubits_number)))
+        if comm is not None:
+            if comm.precision != self._precision:
+                raise ValueError("communicator was created for the other precision library")
+            check(self._lib.qdc_circuit_new_sharded(C.byref(h), int(qubits_number), comm.handle))
+        elif local_shards is not None:
+            check(self._lib.qdc_circuit_new_local_shards(C.byref(h), int(qubits_number),
+                                                         int(local_shards)))
+        else:
+            check(self._lib.qdc_circuit_new(C.byref(h), int(qubits_number)))
+        self._comm = comm  # keep the communicator alive as long as the circuit
         self._h = h
         self._n = int(qubits_number)
         self._kinds = []  # instruction kinds, for splitting the flat outputs
@@ -171,11 +184,36 @@ class _CircuitBase:
                 if k in (VAR_Q1, VAR_Q1_NONU, VAR_Q2, VAR_Q2_NONU, VAR_Q2_DIAG)]
 
     # --- extras (not in the reference's Python surface) --------------------------------
-    def get_state(self, which: int = 0) -> np.ndarray:
-        """Copy of the forward (0), initial (1) or backward (2) device state."""
-        out = np.empty(1 << self._n, dtype=self._dtype)
-        check(self._lib.qdc_circuit_get_state(self._h, which, ptr(out), out.size))
+    def layout(self):
+        """(phys, world, first_rank, local_shards): phys[q] = physical bit of logical qubit q."""
+        phys = (C.c_uint * self._n)()
+        w, r, ls = C.c_int(), C.c_int(), C.c_int()
+        check(self._lib.qdc_circuit_layout(self._h, phys, C.byref(w), C.byref(r), C.byref(ls)))
+        return list(phys), w.value, r.value, ls.value
+
+    def get_shard(self, which: int = 0, shard: int = 0) -> np.ndarray:
+        phys, world, _, _ = self.layout()
+        out = np.empty(1 << (self._n - (world.bit_length() - 1)), dtype=self._dtype)
+        check(self._lib.qdc_circuit_get_shard(self._h, which, shard, ptr(out), out.size))
         return out
+
+    def get_state(self, which: int = 0) -> np.ndarray:
+        """Copy of the forward (0), initial (1) or backward (2) state in logical qubit order.
+        Sharded over processes: the local shards are gathered with torch.distributed."""
+        phys, world, rank0, nlocal = self.layout()
+        if world == 1:
+            out = np.empty(1 << self._n, dtype=self._dtype)
+            check(self._lib.qdc_circuit_get_state(self._h, which, ptr(out), out.size))
+            return out
+        shards = [self.get_shard(which, s) for s in range(nlocal)]
+        if nlocal < world:
+            import torch.distributed as dist  # plumbing only
+            got = [None] * world
+            dist.all_gather_object(got, shards[0])
+            shards = got
+        if which == 1:
+            phys = list(range(self._n))  # `initial` is always in the identity layout
+        return unpermute(np.concatenate(shards), phys)
 
     def synchronize(self):
         check(self._lib.qdc_circuit_sync(self._h))
@@ -209,6 +247,40 @@ def circuit_class(precision: str | None = None):
 
 
 Circuit = circuit_class()
+
+
+def unpermute(physical: np.ndarray, phys) -> np.ndarray:
+    """Reorder a state stored in a physical layout (rank bits on top) into logical qubit order."""
+    n = len(phys)
+    t = physical.reshape((2,) * n)  # axis k <-> physical bit n-1-k
+    axes = [n - 1 - phys[n - 1 - k] for k in range(n)]  # logical axis k = qubit n-1-k
+    return np.ascontiguousarray(t.transpose(axes)).reshape(-1)
+
+
+def plan(qubits_number, world, instructions, mode, start_phys=None, precision=None):
+    """The sharding planner of the native runtime (qdc_plan, host only): returns
+    (ops, end_phys); ops are dicts {"type": "op"|"remap", ...}.  mode: 0 run, 1 forward,
+    2 backward.  `instructions` = [(kind, pos2[, pos1])]."""
+    lib = load(precision or default_precision())
+    m = len(instructions)
+    kinds = (C.c_int * m)(*[int(i[0]) for i in instructions])
+    a = (C.c_uint * m)(*[int(i[1]) for i in instructions])
+    b = (C.c_uint * m)(*[int(i[2]) if len(i) > 2 else 0 for i in instructions])
+    sp = (C.c_uint * qubits_number)(*start_phys) if start_phys is not None else None
+    cap = 4 * m + 16
+    out = (PlanOp * cap)()
+    end = (C.c_uint * qubits_number)()
+    k = int(lib.qdc_plan(qubits_number, world, kinds, a, b, m, mode, sp, out, cap, end))
+    if k == 0 and m > 0:
+        raise ValueError("planner rejected the configuration")
+    ops = []
+    for i in range(min(k, cap)):
+        o = out[i]
+        if o.type == 0:
+            ops.append({"type": "op", "instr": o.instr, "pos2": o.pos2, "pos1": o.pos1})
+        else:
+            ops.append({"type": "remap", "victims": list(o.victims[:o.nvictims]), "pack": bool(o.pack)})
+    return ops, list(end)
 
 
 # ---------------------------------------------------------------------------------------

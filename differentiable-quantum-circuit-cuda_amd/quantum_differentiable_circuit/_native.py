@@ -30,13 +30,21 @@ RUNTIME = (
     "qdc_circuit_set_state_from_vector", "qdc_circuit_push", "qdc_circuit_len",
     "qdc_circuit_output_size", "qdc_circuit_grad_size", "qdc_circuit_execute",
     "qdc_circuit_backward", "qdc_circuit_get_state", "qdc_circuit_sync", "qdc_circuit_profile",
-    "qdc_circuit_profile_collect", "qdc_build_info",
+    "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
+    "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
+    "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_plan",
 )
 
 
 class PanicException(BaseException):
     """Raised where the reference's Rust code panics (PyO3 surfaces those as
     ``pyo3_runtime.PanicException``, a ``BaseException``)."""
+
+
+class PlanOp(C.Structure):
+    """qdc_plan_op (include/qdc/circuit.h)."""
+    _fields_ = [("type", C.c_int), ("instr", C.c_int), ("pos2", C.c_uint), ("pos1", C.c_uint),
+                ("victims", C.c_uint * 8), ("nvictims", C.c_uint), ("pack", C.c_int)]
 
 
 class KernelStat(C.Structure):
@@ -84,6 +92,17 @@ def _proto(lib):
         "qdc_circuit_profile": (_E, [_P, C.c_int]),
         "qdc_circuit_profile_collect": (_S, [_P, C.POINTER(KernelStat), _S]),
         "qdc_build_info": (C.c_char_p, []),
+        "qdc_comm_unique_id": (_E, [C.c_char_p]),
+        "qdc_comm_init": (_E, [C.POINTER(_P), C.c_int, C.c_int, C.c_char_p]),
+        "qdc_comm_free": (None, [_P]),
+        "qdc_circuit_new_sharded": (_E, [C.POINTER(_P), _S, _P]),
+        "qdc_circuit_new_local_shards": (_E, [C.POINTER(_P), _S, C.c_int]),
+        "qdc_circuit_layout": (_E, [_P, C.POINTER(C.c_uint), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "qdc_circuit_get_shard": (_E, [_P, C.c_int, C.c_int, _P, _S]),
+        "qdc_plan": (_S, [_S, _S, C.POINTER(C.c_int), C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                          _S, C.c_int, C.POINTER(C.c_uint), C.POINTER(PlanOp), _S,
+                          C.POINTER(C.c_uint)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

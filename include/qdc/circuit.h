@@ -113,6 +113,51 @@ size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out, size_t 
 /* Library build information: "f32"/"f64", offload arch. */
 const char* qdc_build_info(void);
 
+/* ---- sharded state (no reference counterpart) -------------------------
+ * The 2^n state splits over G = 2^g ranks by its high (physical) qubits.  A qubit map tracks
+ * which logical qubit sits at which physical bit; an op that needs a global qubit is preceded
+ * by a REMAP: one all-to-all per state that swaps all g global qubits with g local ones.
+ * Densities and gradients are summed over ranks (one all-reduce per call), so every rank
+ * returns the full results.  Two transports:
+ *   - qdc_circuit_new_sharded: one shard per process, RCCL over xGMI (qdc_comm_*);
+ *   - qdc_circuit_new_local_shards: every shard on the current GPU, exchanged with device
+ *     copies (the same data path on one GPU; used by the single-GPU parity tests). */
+typedef struct qdc_comm qdc_comm;
+/* rank 0 creates the id and ships it to the other ranks (e.g. torch.distributed broadcast) */
+const char* qdc_comm_unique_id(unsigned char id[128]);
+/* collective over all ranks; uses the current HIP device */
+const char* qdc_comm_init(qdc_comm** out, int rank, int world, const unsigned char id[128]);
+void qdc_comm_free(qdc_comm* comm);
+
+const char* qdc_circuit_new_sharded(qdc_circuit** out, size_t qubits_number, qdc_comm* comm);
+const char* qdc_circuit_new_local_shards(qdc_circuit** out, size_t qubits_number, int shards);
+
+/* Current layout of the forward state: phys[q] = physical bit of logical qubit q (n entries),
+ * plus world size, this process's first rank and its number of local shards. */
+const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world, int* rank,
+                               int* local_shards);
+/* Copy of one local shard (2^(n-g) amplitudes, physical order). which: 0 fwd, 1 initial, 2 bwd */
+const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard, qdc_complex* host,
+                                  size_t len);
+
+/* ---- the sharding planner (host only, no GPU) ---------------------------------------- */
+enum qdc_plan_mode { QDC_PLAN_RUN = 0, QDC_PLAN_FORWARD = 1, QDC_PLAN_BACKWARD = 2 };
+enum qdc_plan_type { QDC_PLAN_OP = 0, QDC_PLAN_REMAP = 1 };
+typedef struct qdc_plan_op {
+  int type;             /* QDC_PLAN_OP: run instruction `instr` at physical (pos2, pos1) */
+  int instr;            /* QDC_PLAN_REMAP: all-to-all with these local victims -> rank bits */
+  unsigned pos2, pos1;
+  unsigned victims[8];  /* ascending; victim j becomes rank bit j */
+  unsigned nvictims;
+  int pack;             /* victims are not the top local bits: pack before the all-to-all */
+} qdc_plan_op;
+/* Plan one pass of `count` instructions over `world` ranks, starting from `start_phys`
+ * (NULL = identity).  Writes at most `cap` ops, returns the total; `end_phys` (nullable)
+ * receives the final layout. */
+size_t qdc_plan(size_t qubits_number, size_t world, const int* kinds, const unsigned* pos2,
+                const unsigned* pos1, size_t count, int mode, const unsigned* start_phys,
+                qdc_plan_op* out, size_t cap, unsigned* end_phys);
+
 #ifdef __cplusplus
 }
 #endif
