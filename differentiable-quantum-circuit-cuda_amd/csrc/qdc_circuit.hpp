@@ -174,6 +174,12 @@ struct Circuit {
   cx* host_out = nullptr;  // pinned
   size_t host_cap = 0;
   std::vector<Instr> ins;
+  // fused multi-gate passes
+  int fuse = 1;             // 0: one HBM pass per gate
+  uint32_t fuse_max_ops = FMAX_OPS;
+  unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
+  unsigned char* prog_host = nullptr;  // pinned staging
+  size_t prog_cap = 0;
 
   // world = total shards (power of two), nlocal = shards in this process
   const char* init(uint32_t qubits, int world = 1, int rank0 = 0, int nlocal = 1,
@@ -190,6 +196,7 @@ struct Circuit {
     ex.nlocal = nlocal;
     ex.comm = comm;
     layout.identity(n, g);
+    if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
     int dev = 0;
     QDC_HIP(hipGetDevice(&dev));
     QDC_TRY(ctx.init(dev));
@@ -217,6 +224,9 @@ struct Circuit {
     sh.clear();
     if (host_out) (void)hipHostFree(host_out);
     host_out = nullptr;
+    if (prog_dev) (void)hipFree(prog_dev);
+    if (prog_host) (void)hipHostFree(prog_host);
+    prog_dev = prog_host = nullptr;
     ctx.destroy();
   }
 
@@ -372,6 +382,232 @@ struct Circuit {
     return out;
   }
 
+  // --- fusion: consecutive gate ops whose qubits fit one tile run as one HBM pass ----------
+  struct Item {
+    int type;          // 0: one plan op, 1: remap, 2: fused group
+    size_t first = 0;  // plan index (type 0/1) or first op of the group (type 2)
+    size_t count = 1;
+    uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {0, 0, 0, 0, 0};
+    size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
+    uint32_t ngrad = 0;
+  };
+  static constexpr uint32_t TILE_CHUNKS_1 = 2048;  // one-state fused tile (chunks)
+  static constexpr uint32_t TILE_CHUNKS_2 = 1024;  // two-state fused tile (chunks per state)
+
+  uint32_t chunk_bits_of(uint32_t p) const { return p >= (uint32_t)LV ? 1u << (p - LV) : 0u; }
+  // the largest contiguous part lc such that the remaining bits fit as <= FMAX_ROWS row bits
+  bool tile_config(uint64_t mask, uint32_t T, uint32_t& lc, uint32_t& h, uint32_t* hb) const {
+    const uint32_t cbits = nl - LV;
+    const uint32_t teff = cbits < T ? cbits : T;
+    const uint32_t lmin = teff < (uint32_t)LOWBITS ? teff : (uint32_t)LOWBITS;
+    for (int l = (int)teff; l >= (int)lmin; --l) {
+      uint32_t rows = 0, tmp[64];
+      for (uint32_t c = (uint32_t)l; c < cbits; ++c)
+        if (mask >> c & 1ull) tmp[rows++] = c;
+      if (rows <= (uint32_t)FMAX_ROWS && (uint32_t)l + rows <= teff) {
+        lc = (uint32_t)l;
+        h = rows;
+        for (uint32_t k = 0; k < rows; ++k) hb[k] = tmp[k];
+        return true;
+      }
+    }
+    return false;
+  }
+
+  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward) const {
+    std::vector<Item> items;
+    size_t gfirst = 0, gcount = 0;
+    uint64_t gmask = 0;
+    uint32_t ggrad = 0;
+    auto close = [&]() {
+      if (gcount >= 2) {
+        Item it{2, gfirst, gcount};
+        const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
+        tile_config(gmask, T, it.lc, it.h, it.hb);
+        it.ngrad = ggrad;
+        items.push_back(it);
+      } else if (gcount == 1) {
+        items.push_back(Item{0, gfirst, 1});
+      }
+      gcount = 0;
+      gmask = 0;
+      ggrad = 0;
+    };
+    const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
+    for (size_t i = 0; i < plan.size(); ++i) {
+      const qdc_plan_op& op = plan[i];
+      if (op.type == QDC_PLAN_REMAP) {
+        close();
+        items.push_back(Item{1, i, 1});
+        continue;
+      }
+      const Instr& in = ins[op.instr];
+      const bool gate = is_const(in.kind) || is_var(in.kind);
+      if (!gate || !fuse || fuse_max_ops < 2) {
+        close();
+        items.push_back(Item{0, i, 1});
+        continue;
+      }
+      const uint64_t bits = chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
+      const uint32_t isgrad = (backward && is_var(in.kind)) ? 1u : 0u;
+      uint32_t lc, h, hb[FMAX_ROWS];
+      if (gcount > 0 && gcount < fuse_max_ops && ggrad + isgrad <= (uint32_t)FIN_MAX &&
+          tile_config(gmask | bits, T, lc, h, hb)) {
+        gmask |= bits;
+        ++gcount;
+        ggrad += isgrad;
+        continue;
+      }
+      close();
+      if (tile_config(bits, T, lc, h, hb)) {
+        gfirst = i;
+        gcount = 1;
+        gmask = bits;
+        ggrad = isgrad;
+      } else {
+        items.push_back(Item{0, i, 1});
+      }
+    }
+    close();
+    return items;
+  }
+
+  // Lay out every fused group's fop array and matrices in one pinned buffer, then upload it.
+  // backward: `first_inject` = plan index of the first cotangent injection (groups before it
+  // only uncompute fwd).
+  const char* build_program(std::vector<Item>& items, const std::vector<qdc_plan_op>& plan,
+                            bool backward, size_t first_inject, const Flat& cg, const Flat& vg,
+                            const std::vector<size_t>& gidx, size_t& mats_off) {
+    size_t nops = 0, nmat = 0;
+    for (auto& it : items)
+      if (it.type == 2) {
+        nops += it.count;
+        nmat += it.count * 32;
+      }
+    if (nops == 0) return nullptr;
+    mats_off = ((nops * sizeof(fop) + 255) / 256) * 256;
+    const size_t bytes = mats_off + nmat * sizeof(cx);
+    if (bytes > prog_cap) {
+      QDC_HIP(hipStreamSynchronize(ctx.stream));
+      if (prog_dev) QDC_HIP(hipFree(prog_dev));
+      if (prog_host) QDC_HIP(hipHostFree(prog_host));
+      prog_dev = prog_host = nullptr;
+      QDC_HIP(hipMalloc(&prog_dev, bytes));
+      QDC_HIP(hipHostMalloc(&prog_host, bytes));
+      prog_cap = bytes;
+    }
+    fop* fops = reinterpret_cast<fop*>(prog_host);
+    cx* mats = reinterpret_cast<cx*>(prog_host + mats_off);
+    size_t fo = 0, mo = 0;
+    for (auto& it : items) {
+      if (it.type != 2) continue;
+      it.fop_off = fo * sizeof(fop);
+      const bool two = backward && it.first > first_inject;
+      for (size_t k = 0; k < it.count; ++k) {
+        const qdc_plan_op& op = plan[it.first + k];
+        const Instr& in = ins[op.instr];
+        const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
+        auto local_bit = [&](uint32_t p) -> uint32_t {
+          if (p < (uint32_t)LV + it.lc) return p;
+          for (uint32_t r = 0; r < it.h; ++r)
+            if (it.hb[r] == p - LV) return LV + it.lc + r;
+          return 0xffffffffu;  // unreachable: tile_config covered every bit
+        };
+        fop& F = fops[fo++];
+        F.t2 = local_bit(op.pos2);
+        F.t1 = local_bit(op.pos1);
+        F.mat = (uint32_t)mo;
+        const bool grad = two && is_var(in.kind);
+        if (is_diag(in.kind)) {
+          F.kind = 2 | (grad ? 4u : 0u);
+          const diag4 d = to_diag(g4);
+          const diag4 a = backward ? conj_diag(d) : d;
+          for (int i = 0; i < 4; ++i) mats[mo + i] = a.a[i];
+          for (int i = 0; i < 4; ++i) mats[mo + 4 + i] = d.a[i];
+          mo += 8;
+        } else if (is_q1_gate(in.kind)) {
+          F.kind = 0 | (grad ? 4u : 0u);
+          const mat<2> u = to_mat<2>(g4);
+          mat<2> a = u;
+          if (backward) {
+            if (is_nonu(in.kind))
+              QDC_TRY(inverse<2>(u, a));
+            else
+              a = conj_transpose<2>(u);
+          }
+          const mat<2> bt = transpose<2>(u);
+          for (int i = 0; i < 4; ++i) mats[mo + i] = a.a[i];
+          for (int i = 0; i < 4; ++i) mats[mo + 4 + i] = bt.a[i];
+          mo += 8;
+        } else {
+          F.kind = 1 | (grad ? 4u : 0u);
+          const mat<4> u = to_mat<4>(g4);
+          mat<4> a = u;
+          if (backward) {
+            if (is_nonu(in.kind))
+              QDC_TRY(inverse<4>(u, a));
+            else
+              a = conj_transpose<4>(u);
+          }
+          const mat<4> bt = transpose<4>(u);
+          for (int i = 0; i < 16; ++i) mats[mo + i] = a.a[i];
+          for (int i = 0; i < 16; ++i) mats[mo + 16 + i] = bt.a[i];
+          mo += 32;
+        }
+      }
+    }
+    QDC_HIP(hipMemcpyAsync(prog_dev, prog_host, mats_off + mo * sizeof(cx),
+                           hipMemcpyHostToDevice, ctx.stream));
+    return nullptr;
+  }
+
+  // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
+  // gradient gates write partials for gradient buffer rows var_idx[...].
+  const char* run_fused(const Item& it, const std::vector<qdc_plan_op>& plan, bool two,
+                        size_t mats_off, const std::vector<uint32_t>& var_idx) {
+    fgeo fg{};
+    fg.lc = it.lc;
+    fg.h = it.h;
+    for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];
+    fg.nops = (uint32_t)it.count;
+    fg.ngrad = two ? it.ngrad : 0;
+    fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
+    const uint32_t target = two ? ctx.red_cap : ctx.grid_cap;
+    uint64_t tpb = 1;
+    while (tpb * target < fg.ntiles) tpb <<= 1;
+    fg.tpb = (uint32_t)tpb;
+    const uint32_t grid = (uint32_t)((fg.ntiles + tpb - 1) / tpb);
+    const fop* fops = reinterpret_cast<const fop*>(prog_dev + it.fop_off);
+    const cx* mats = reinterpret_cast<const cx*>(prog_dev + mats_off);
+    const double bytes = (two ? 4.0 : 2.0) * state_bytes(nl);
+    for (auto& s : sh) {
+      chunk* f = reinterpret_cast<chunk*>(s.state);
+      chunk* b = reinterpret_cast<chunk*>(s.bwd);
+      if (!two) {
+        QDC_TRY(ctx.launch("fused_apply", bytes, k_fused<false, TILE_CHUNKS_1>, grid, f, b, fops,
+                           mats, fg, (cx*)nullptr, (uint64_t)0));
+        continue;
+      }
+      if (fg.ngrad == 0) {
+        QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
+                           mats, fg, (cx*)nullptr, (uint64_t)0));
+        continue;
+      }
+      if (grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
+      QDC_TRY(ctx.begin_reduction(s.grads, 0));
+      if (ctx.pending_dst.size() + fg.ngrad > (size_t)FIN_MAX) QDC_TRY(ctx.flush());
+      ctx.pending_base = s.grads;
+      ctx.pending_accumulate = 0;
+      QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
+                         mats, fg, ctx.slot_ptr(), (uint64_t)NBMAX * RED));
+      for (size_t k = 0; k < it.count; ++k) {
+        const Instr& in = ins[plan[it.first + k].instr];
+        if (is_var(in.kind)) ctx.commit(var_idx[plan[it.first + k].instr], grid);
+      }
+    }
+    return nullptr;
+  }
+
   // --- forward (Circuit::run / Circuit::forward) --------------------------------------------
   const char* apply_gate(const Instr& in, const qdc_complex* g4, cx* s, uint32_t p2, uint32_t p1,
                          bool uncompute) {
@@ -417,7 +653,16 @@ struct Circuit {
         if (is_diff_density(ins[k].kind) || (mode == QDC_MODE_RUN && is_density(ins[k].kind)))
           out_idx[k] = o++;
     }
-    for (const qdc_plan_op& op : plan(mode)) {
+    const std::vector<qdc_plan_op> pl = plan(mode);
+    std::vector<Item> items = fuse_items(pl, false);
+    size_t mats_off = 0;
+    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off));
+    for (const Item& item : items) {
+      if (item.type == 2) {
+        QDC_TRY(run_fused(item, pl, false, mats_off, {}));
+        continue;
+      }
+      const qdc_plan_op& op = pl[item.first];
       if (op.type == QDC_PLAN_REMAP) {
         QDC_TRY(remap(op, false));
         continue;
@@ -485,7 +730,22 @@ struct Circuit {
         if (is_var(ins[k].kind)) var_idx[k] = v++;
     }
     bool have_bwd = false;
-    for (const qdc_plan_op& op : plan(QDC_PLAN_BACKWARD)) {
+    const std::vector<qdc_plan_op> pl = plan(QDC_PLAN_BACKWARD);
+    size_t first_inject = pl.size();
+    for (size_t i = 0; i < pl.size(); ++i)
+      if (pl[i].type == QDC_PLAN_OP && is_diff_density(ins[pl[i].instr].kind)) {
+        first_inject = i;
+        break;
+      }
+    std::vector<Item> items = fuse_items(pl, true);
+    size_t mats_off = 0;
+    QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off));
+    for (const Item& item : items) {
+      if (item.type == 2) {
+        QDC_TRY(run_fused(item, pl, have_bwd, mats_off, var_idx));
+        continue;
+      }
+      const qdc_plan_op& op = pl[item.first];
       if (op.type == QDC_PLAN_REMAP) {
         QDC_TRY(remap(op, have_bwd));
         continue;

@@ -536,6 +536,275 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// FUSED family: a run of consecutive gates whose qubits all fit one
+// tile is applied in ONE HBM pass.  A tile = TB chunks of each state: `lc` contiguous low
+// chunk bits (>= 6: every wave instruction stays on a contiguous KiB) plus `h` row bits at
+// far chunk positions hb[].  The gates run one after the other on LDS (a barrier between
+// gates); a two-state (reverse) program uncomputes fwd, accumulates each variable gate's
+// gradient and pulls bwd back, exactly as k_direct / k_tile do for one gate.
+// Gradients: per thread in registers during a gate, then a reduce-scatter butterfly over the
+// wave (~V shuffles for V values instead of 6V) and one LDS add per value into the wave's
+// accumulator slot for that gate; one partial per block and gate at the end.
+// ---------------------------------------------------------------------------------------
+constexpr int FMAX_OPS = 16;   // gates per fused pass
+constexpr int FMAX_ROWS = 5;   // far qubits per tile
+constexpr int FACC = 32;       // reals per gradient accumulator (16 complex)
+
+struct fop {
+  uint32_t kind;  // 0: one-qubit dense, 1: two-qubit dense, 2: two-qubit diagonal; +4: gradient
+  uint32_t t1;    // tile-local amplitude bit of pos1 (one-qubit: the target)
+  uint32_t t2;    // tile-local amplitude bit of pos2
+  uint32_t mat;   // offset (complex) of A in the matrix buffer; B follows (R^2, or 4 for diag)
+};
+
+struct fgeo {
+  uint64_t ntiles;
+  uint32_t tpb;    // tiles per block (block-contiguous)
+  uint32_t lc;     // contiguous chunk bits
+  uint32_t h;      // row bits
+  uint32_t hb[FMAX_ROWS];
+  uint32_t nops;
+  uint32_t ngrad;  // gradient gates (their partials go to consecutive slots)
+};
+
+// Lane select with a wave-uniform lane mask (v_cndmask): lanes set in `mask` take t.  Written
+// as asm because LLVM folds `upper ? x[h + i] : x[i]` on a register array into a dynamically
+// indexed array (a compare/select chain over every element: O(V^2) instructions).
+__device__ __forceinline__ uint32_t lane_sel(uint32_t f, uint32_t t, uint64_t mask) {
+  uint32_t r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mask));
+  return r;
+}
+__device__ __forceinline__ float lane_sel(float f, float t, uint64_t mask) {
+  return __uint_as_float(lane_sel(__float_as_uint(f), __float_as_uint(t), mask));
+}
+__device__ __forceinline__ double lane_sel(double f, double t, uint64_t mask) {
+  const uint64_t fb = (uint64_t)__double_as_longlong(f), tb = (uint64_t)__double_as_longlong(t);
+  const uint64_t lo = lane_sel((uint32_t)fb, (uint32_t)tb, mask);
+  const uint64_t hi = lane_sel((uint32_t)(fb >> 32), (uint32_t)(tb >> 32), mask);
+  return __longlong_as_double((long long)(lo | (hi << 32)));
+}
+
+// Sum V reals over the 64 lanes; lanes whose low (6 - log2 V) index bits are zero end up
+// holding value idx(lane), and add it into acc[idx] (acc in LDS, one writer per index).
+template <int V>
+__device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
+  // lanes with bit o of the lane id set, o = 32, 16, ..., 1
+  constexpr uint64_t UPPER[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull,
+                                 0xFF00FF00FF00FF00ull, 0xF0F0F0F0F0F0F0F0ull,
+                                 0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};
+  const int lane = threadIdx.x & 63;
+  int idx = 0;
+  // reduce-scatter steps: offsets 32, 16, ... while more than one value remains; the upper
+  // half of each lane pair keeps values [half, len), the lower half keeps [0, half)
+#pragma unroll
+  for (int step = 0; step < 6; ++step) {
+    const int o = 32 >> step;
+    const int len = V >> step;
+    if (len > 1) {
+      const int half = len >> 1;
+#pragma unroll
+      for (int i = 0; i < half; ++i) {
+        const real mine = lane_sel(x[i], x[half + i], UPPER[step]);
+        const real send = lane_sel(x[half + i], x[i], UPPER[step]);
+        x[i] = mine + __shfl_xor(send, o, 64);
+      }
+      idx += (lane & o) ? half : 0;
+    } else {
+      x[0] += __shfl_xor(x[0], o, 64);
+    }
+  }
+  const int spread = 64 / V;  // lanes holding the same idx
+  if ((lane & (spread - 1)) == 0) acc[idx] += x[0];
+}
+
+template <bool TWO, int TB>
+__global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                 const fop* __restrict__ ops,
+                                                 const cx* __restrict__ mats, fgeo fg,
+                                                 cx* __restrict__ partials,
+                                                 uint64_t slot_stride) {
+  constexpr int NS = TWO ? 2 : 1;
+  __shared__ chunk lds[NS][TB];
+  __shared__ real accw[BLOCK / 64][FMAX_OPS][FACC];
+  const uint32_t t = threadIdx.x;
+  const int wave = t >> 6;
+  if constexpr (TWO) {
+    for (uint32_t i = t; i < (BLOCK / 64) * FMAX_OPS * FACC; i += BLOCK)
+      (&accw[0][0][0])[i] = 0;
+  }
+  const uint32_t tc = 1u << (fg.lc + fg.h);  // chunks per tile (== TB except tiny states)
+  const uint32_t ta = tc * VEC;              // amplitudes per tile
+  cx* lf = reinterpret_cast<cx*>(&lds[0][0]);
+  cx* lb = reinterpret_cast<cx*>(&lds[NS - 1][0]);
+  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
+  for (uint32_t tt = 0; tt < fg.tpb; ++tt) {
+    const uint64_t tile = tile0 + tt;
+    if (tile >= fg.ntiles) break;
+    uint64_t base = tile << fg.lc;
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
+    auto gidx = [&](uint32_t c) {
+      uint64_t gi = base + (c & ((1u << fg.lc) - 1u));
+#pragma unroll
+      for (int k = 0; k < FMAX_ROWS; ++k)
+        if ((uint32_t)k < fg.h) gi += (uint64_t)((c >> (fg.lc + k)) & 1u) << fg.hb[k];
+      return gi;
+    };
+    for (uint32_t c = t; c < tc; c += BLOCK) {
+      const uint64_t gi = gidx(c);
+      lds[0][c] = ldc(f + gi);
+      if constexpr (TWO) lds[1][c] = ldc(b + gi);
+    }
+    __syncthreads();
+    uint32_t gi_op = 0;
+    for (uint32_t j = 0; j < fg.nops; ++j) {
+      const fop op = ops[j];
+      const uint32_t kind = op.kind & 3u;
+      const bool grad = TWO && (op.kind & 4u);
+      const cx* M = mats + op.mat;
+      if (kind == 0) {  // one-qubit dense
+        mat<2> A, B;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A.a[i] = M[i];
+        if constexpr (TWO) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) B.a[i] = M[4 + i];
+        }
+        cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        const uint32_t s1 = 1u << op.t1;
+        for (uint32_t grp = t; grp < ta / 2; grp += BLOCK) {
+          const uint32_t a0 = (uint32_t)insert_zero(grp, op.t1);
+          cx fx[2] = {lf[a0], lf[a0 + s1]};
+          if constexpr (TWO) {
+            cx bx[2] = {lb[a0], lb[a0 + s1]};
+            if (grad)
+              op_vector<OP_REVERSE_GRAD, 2>(A, B, fx, bx, acc);
+            else
+              op_vector<OP_REVERSE, 2>(A, B, fx, bx, acc);
+            lb[a0] = bx[0];
+            lb[a0 + s1] = bx[1];
+          } else {
+            matvec<2>(A, fx);
+          }
+          lf[a0] = fx[0];
+          lf[a0 + s1] = fx[1];
+        }
+        if (grad) {
+          real v[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[2 * i] = acc[i].x;
+            v[2 * i + 1] = acc[i].y;
+          }
+          wave_reduce_add<8>(v, &accw[wave][gi_op][0]);
+        }
+      } else if (kind == 1) {  // two-qubit dense
+        mat<4> A, B;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) A.a[i] = M[i];
+        if constexpr (TWO) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) B.a[i] = M[16 + i];
+        }
+        cx acc[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = {0, 0};
+        const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
+        const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
+        const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
+        for (uint32_t grp = t; grp < ta / 4; grp += BLOCK) {
+          const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
+          const uint32_t off[4] = {0, s1, s2, s1 + s2};
+          cx fx[4], bx[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) fx[r] = lf[a0 + off[r]];
+          if constexpr (TWO) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bx[r] = lb[a0 + off[r]];
+            if (grad)
+              op_vector<OP_REVERSE_GRAD, 4>(A, B, fx, bx, acc);
+            else
+              op_vector<OP_REVERSE, 4>(A, B, fx, bx, acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lb[a0 + off[r]] = bx[r];
+          } else {
+            matvec<4>(A, fx);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lf[a0 + off[r]] = fx[r];
+        }
+        if (grad) {
+          real v[32];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            v[2 * i] = acc[i].x;
+            v[2 * i + 1] = acc[i].y;
+          }
+          wave_reduce_add<32>(v, &accw[wave][gi_op][0]);
+        }
+      } else {  // two-qubit diagonal: A = applied diagonal (uncompute: conj), B = d
+        // quartets over (pos2, pos1): element r = 2 P2 + P1 takes diagonal entry r (static)
+        cx A[4], B[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A[i] = M[i];
+        if constexpr (TWO) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
+        }
+        cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
+        const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
+        const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
+        for (uint32_t grp = t; grp < ta / 4; grp += BLOCK) {
+          const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
+          const uint32_t off[4] = {0, s1, s2, s1 + s2};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const cx fv = cmul(A[r], lf[a0 + off[r]]);
+            lf[a0 + off[r]] = fv;
+            if constexpr (TWO) {
+              const cx bv = lb[a0 + off[r]];
+              if (grad) acc[r] = cfma(bv, fv, acc[r]);
+              lb[a0 + off[r]] = cmul(B[r], bv);
+            }
+          }
+        }
+        if (grad) {
+          real v[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[2 * i] = acc[i].x;
+            v[2 * i + 1] = acc[i].y;
+          }
+          wave_reduce_add<8>(v, &accw[wave][gi_op][0]);
+        }
+      }
+      gi_op += grad ? 1u : 0u;
+      __syncthreads();
+    }
+    for (uint32_t c = t; c < tc; c += BLOCK) {
+      const uint64_t gi = gidx(c);
+      stc(f + gi, lds[0][c]);
+      if constexpr (TWO) stc(b + gi, lds[1][c]);
+    }
+    __syncthreads();  // the next tile overwrites lds
+  }
+  if constexpr (TWO) {
+    // one partial (16 complex) per block and gradient gate: slot k at partials + k*slot_stride
+    for (uint32_t i = t; i < fg.ngrad * FACC; i += BLOCK) {
+      const uint32_t k = i / FACC, e = i % FACC;
+      real s = 0;
+#pragma unroll
+      for (int w = 0; w < BLOCK / 64; ++w) s += accw[w][k][e];
+      reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] = s;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Remap pack (qdc_shard.hpp): dst block j (victim bit pattern j) = the source chunks whose
 // victim bits equal j, in order.  dst[o] = src[expand(o)]: insert zeros at the victim chunk

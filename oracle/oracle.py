@@ -457,6 +457,44 @@ def autodiff_circuit(n, layers, seed):
     return ins, const, var, pert
 
 
+def random_circuit(n, ngates, seed, density_every=0):
+    """A random circuit over every gate kind on arbitrary (non-adjacent, either order) qubit
+    pairs — the random-circuit configuration of SURVEY.md §8 d (C5), also used to exercise the
+    runtime's multi-gate fusion.  Every `density_every` gates (0: never) a DiffQ1Density or
+    DiffQ2Density on random qubits; DiffQ1Density on every qubit at the end.
+    Returns (ins, const_gates, var_gates)."""
+    rng = np.random.default_rng(seed)
+    ins, const, var = [], [], []
+    kinds = [CONST_Q2, VAR_Q2, CONST_Q2_NONU, VAR_Q2_NONU, CONST_Q2_DIAG, VAR_Q2_DIAG,
+             CONST_Q1, CONST_Q1_NONU, VAR_Q1, VAR_Q1_NONU]
+    for i in range(ngates):
+        k = kinds[rng.integers(len(kinds))]
+        if k in (CONST_Q1, CONST_Q1_NONU, VAR_Q1, VAR_Q1_NONU):
+            ins.append((k, (int(rng.integers(n)),)))
+            g = haar_unitary(rng, 2)
+            if k in (CONST_Q1_NONU, VAR_Q1_NONU):
+                g = g + 0.05 * (rng.standard_normal(4) + 1j * rng.standard_normal(4))
+        else:
+            a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+            ins.append((k, (a, b)))
+            if k in (CONST_Q2_DIAG, VAR_Q2_DIAG):
+                g = np.exp(1j * rng.standard_normal(4))
+            else:
+                g = haar_unitary(rng, 4)
+                if k in (CONST_Q2_NONU, VAR_Q2_NONU):
+                    g = g + 0.05 * (rng.standard_normal(16) + 1j * rng.standard_normal(16))
+        (const if k in (CONST_Q2, CONST_Q2_NONU, CONST_Q2_DIAG, CONST_Q1, CONST_Q1_NONU)
+         else var).append(g)
+        if density_every and (i + 1) % density_every == 0:
+            if rng.integers(2):
+                ins.append((DIFF_Q1_DENSITY, (int(rng.integers(n)),)))
+            else:
+                a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+                ins.append((DIFF_Q2_DENSITY, (a, b)))
+    ins += [(DIFF_Q1_DENSITY, (q,)) for q in range(n)]
+    return ins, const, var
+
+
 def tsallis_loss_and_cotangents(densities):
     """av_tsallis of test_autodiff.py:87-92: mean over densities of 1 - tr(rho^2).
     Returns (loss, JAX cotangents d loss / d rho) — the holomorphic derivative -2 rho^T / N,
