@@ -177,6 +177,9 @@ struct Circuit {
   // fused multi-gate passes
   int fuse = 1;             // 0: one HBM pass per gate
   uint32_t fuse_max_ops = FMAX_OPS;
+  uint32_t fuse_lcmin = LOWBITS;  // min contiguous chunk bits of a fused tile
+  uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
+  uint32_t fused_resident[2] = {0, 0};
   unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
   unsigned char* prog_host = nullptr;  // pinned staging
   size_t prog_cap = 0;
@@ -197,6 +200,12 @@ struct Circuit {
     ex.comm = comm;
     layout.identity(n, g);
     if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
+    if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
+      fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
+    if (const char* e = getenv("QDC_FUSE_LCMIN"))
+      fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
+    if (const char* e = getenv("QDC_FUSED_BLOCKS"))
+      fused_blocks = (uint32_t)std::max(1, std::min(atoi(e), (int)NBMAX));
     int dev = 0;
     QDC_HIP(hipGetDevice(&dev));
     QDC_TRY(ctx.init(dev));
@@ -382,93 +391,114 @@ struct Circuit {
     return out;
   }
 
-  // --- fusion: consecutive gate ops whose qubits fit one tile run as one HBM pass ----------
+  // --- fusion: gates whose qubits fit one tile run as one HBM pass ---------------------------
+  // Gates on disjoint qubits commute, so within a segment of consecutive gate ops (bounded by
+  // remaps, densities and cotangent injections) a pass may take any gate none of whose
+  // earlier same-qubit gates is left for a later pass.  Each pass is built greedily in
+  // program order: a gate joins if it is ready and its qubits still fit the tile, otherwise
+  // its qubits are blocked for the rest of the scan.  Per qubit, gates keep program order, so
+  // the result equals the sequential one up to floating-point rounding.
   struct Item {
-    int type;          // 0: one plan op, 1: remap, 2: fused group
-    size_t first = 0;  // plan index (type 0/1) or first op of the group (type 2)
-    size_t count = 1;
-    uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {0, 0, 0, 0, 0};
+    int type;                    // 0: one plan op, 1: remap, 2: fused group
+    std::vector<uint32_t> ops;   // plan indices (one for type 0/1), program order
+    uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {};
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t ngrad = 0;
   };
   static constexpr uint32_t TILE_CHUNKS_1 = 2048;  // one-state fused tile (chunks)
   static constexpr uint32_t TILE_CHUNKS_2 = 1024;  // two-state fused tile (chunks per state)
 
-  uint32_t chunk_bits_of(uint32_t p) const { return p >= (uint32_t)LV ? 1u << (p - LV) : 0u; }
-  // the largest contiguous part lc such that the remaining bits fit as <= FMAX_ROWS row bits
+  uint64_t chunk_bits_of(uint32_t p) const { return p >= (uint32_t)LV ? 1ull << (p - LV) : 0ull; }
+  // A full tile of 2^T chunks: lc contiguous chunk bits (>= fuse_lcmin) plus h = T - lc row
+  // bits that cover the group's far target bits, padded with the lowest free bits above lc.
+  // States with fewer than 2^T chunks are not fused.
   bool tile_config(uint64_t mask, uint32_t T, uint32_t& lc, uint32_t& h, uint32_t* hb) const {
     const uint32_t cbits = nl - LV;
-    const uint32_t teff = cbits < T ? cbits : T;
-    const uint32_t lmin = teff < (uint32_t)LOWBITS ? teff : (uint32_t)LOWBITS;
-    for (int l = (int)teff; l >= (int)lmin; --l) {
+    if (cbits < T) return false;
+    for (int l = (int)T; l >= (int)fuse_lcmin; --l) {
       uint32_t rows = 0, tmp[64];
       for (uint32_t c = (uint32_t)l; c < cbits; ++c)
         if (mask >> c & 1ull) tmp[rows++] = c;
-      if (rows <= (uint32_t)FMAX_ROWS && (uint32_t)l + rows <= teff) {
-        lc = (uint32_t)l;
-        h = rows;
-        for (uint32_t k = 0; k < rows; ++k) hb[k] = tmp[k];
-        return true;
-      }
+      if (rows > (uint32_t)FMAX_ROWS || (uint32_t)l + rows > T) continue;
+      for (uint32_t c = (uint32_t)l; c < cbits && (uint32_t)l + rows < T; ++c)
+        if (!(mask >> c & 1ull)) tmp[rows++] = c;
+      if ((uint32_t)l + rows != T || rows > (uint32_t)FMAX_ROWS) continue;
+      std::sort(tmp, tmp + rows);
+      lc = (uint32_t)l;
+      h = rows;
+      for (uint32_t k = 0; k < rows; ++k) hb[k] = tmp[k];
+      return true;
+    }
+    return false;
+  }
+  bool tile_fits(uint64_t mask, uint32_t T) const {
+    if (nl - LV < T) return false;
+    for (int l = (int)T; l >= (int)fuse_lcmin; --l) {
+      const uint32_t rows = (uint32_t)__builtin_popcountll(mask >> l);
+      if (rows <= (uint32_t)FMAX_ROWS && (uint32_t)l + rows <= T) return true;
     }
     return false;
   }
 
   std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward) const {
     std::vector<Item> items;
-    size_t gfirst = 0, gcount = 0;
-    uint64_t gmask = 0;
-    uint32_t ggrad = 0;
-    auto close = [&]() {
-      if (gcount >= 2) {
-        Item it{2, gfirst, gcount};
-        const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
-        tile_config(gmask, T, it.lc, it.h, it.hb);
-        it.ngrad = ggrad;
-        items.push_back(it);
-      } else if (gcount == 1) {
-        items.push_back(Item{0, gfirst, 1});
-      }
-      gcount = 0;
-      gmask = 0;
-      ggrad = 0;
-    };
     const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
-    for (size_t i = 0; i < plan.size(); ++i) {
+    auto is_gate = [&](const qdc_plan_op& op) {
+      if (op.type != QDC_PLAN_OP) return false;
+      const Instr& in = ins[op.instr];
+      return is_const(in.kind) || is_var(in.kind);
+    };
+    auto bits_of = [&](const qdc_plan_op& op) {
+      return chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
+    };
+    const bool on = fuse && fuse_max_ops >= 2;
+    size_t i = 0;
+    while (i < plan.size()) {
       const qdc_plan_op& op = plan[i];
       if (op.type == QDC_PLAN_REMAP) {
-        close();
-        items.push_back(Item{1, i, 1});
+        items.push_back(Item{1, {(uint32_t)i}});
+        ++i;
         continue;
       }
-      const Instr& in = ins[op.instr];
-      const bool gate = is_const(in.kind) || is_var(in.kind);
-      if (!gate || !fuse || fuse_max_ops < 2) {
-        close();
-        items.push_back(Item{0, i, 1});
+      if (!on || !is_gate(op) || !tile_fits(bits_of(op), T)) {
+        items.push_back(Item{0, {(uint32_t)i}});
+        ++i;
         continue;
       }
-      const uint64_t bits = chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
-      const uint32_t isgrad = (backward && is_var(in.kind)) ? 1u : 0u;
-      uint32_t lc, h, hb[FMAX_ROWS];
-      if (gcount > 0 && gcount < fuse_max_ops && ggrad + isgrad <= (uint32_t)FIN_MAX &&
-          tile_config(gmask | bits, T, lc, h, hb)) {
-        gmask |= bits;
-        ++gcount;
-        ggrad += isgrad;
-        continue;
+      size_t j = i;
+      while (j < plan.size() && is_gate(plan[j]) && tile_fits(bits_of(plan[j]), T)) ++j;
+      std::vector<uint32_t> rem;
+      for (size_t k = i; k < j; ++k) rem.push_back((uint32_t)k);
+      while (!rem.empty()) {
+        uint64_t mask = 0, blocked = 0;
+        uint32_t ngrad = 0;
+        std::vector<uint32_t> pass, rest;
+        for (uint32_t k : rem) {
+          const qdc_plan_op& g = plan[k];
+          const uint64_t q = (1ull << g.pos2) | (1ull << g.pos1);
+          const uint32_t isgrad = (backward && is_var(ins[g.instr].kind)) ? 1u : 0u;
+          if ((q & blocked) || pass.size() >= fuse_max_ops || ngrad + isgrad > (uint32_t)FMAX_GRAD ||
+              !tile_fits(mask | bits_of(g), T)) {
+            blocked |= q;
+            rest.push_back(k);
+            continue;
+          }
+          pass.push_back(k);
+          mask |= bits_of(g);
+          ngrad += isgrad;
+        }
+        if (pass.size() == 1) {
+          items.push_back(Item{0, pass});
+        } else {
+          Item it{2, pass};
+          tile_config(mask, T, it.lc, it.h, it.hb);
+          it.ngrad = ngrad;
+          items.push_back(it);
+        }
+        rem.swap(rest);
       }
-      close();
-      if (tile_config(bits, T, lc, h, hb)) {
-        gfirst = i;
-        gcount = 1;
-        gmask = bits;
-        ggrad = isgrad;
-      } else {
-        items.push_back(Item{0, i, 1});
-      }
+      i = j;
     }
-    close();
     return items;
   }
 
@@ -481,8 +511,8 @@ struct Circuit {
     size_t nops = 0, nmat = 0;
     for (auto& it : items)
       if (it.type == 2) {
-        nops += it.count;
-        nmat += it.count * 32;
+        nops += it.ops.size();
+        nmat += it.ops.size() * 32;
       }
     if (nops == 0) return nullptr;
     mats_off = ((nops * sizeof(fop) + 255) / 256) * 256;
@@ -502,9 +532,9 @@ struct Circuit {
     for (auto& it : items) {
       if (it.type != 2) continue;
       it.fop_off = fo * sizeof(fop);
-      const bool two = backward && it.first > first_inject;
-      for (size_t k = 0; k < it.count; ++k) {
-        const qdc_plan_op& op = plan[it.first + k];
+      const bool two = backward && it.ops[0] > first_inject;
+      for (uint32_t pi : it.ops) {
+        const qdc_plan_op& op = plan[pi];
         const Instr& in = ins[op.instr];
         const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
         auto local_bit = [&](uint32_t p) -> uint32_t {
@@ -569,10 +599,27 @@ struct Circuit {
     fg.lc = it.lc;
     fg.h = it.h;
     for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];
-    fg.nops = (uint32_t)it.count;
+    fg.nops = (uint32_t)it.ops.size();
     fg.ngrad = two ? it.ngrad : 0;
     fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
-    const uint32_t target = two ? ctx.red_cap : ctx.grid_cap;
+    // one wave of resident blocks, each pipelining a contiguous run of tiles
+    uint32_t target = fused_blocks;
+    if (target == 0) {
+      uint32_t& res = fused_resident[two ? 1 : 0];
+      if (res == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (two)
+          QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &per_cu, k_fused<true, TILE_CHUNKS_2>, BLOCK, 0));
+        else
+          QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &per_cu, k_fused<false, TILE_CHUNKS_1>, BLOCK, 0));
+        QDC_HIP(hipGetDevice(&dev));
+        QDC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        res = (uint32_t)std::max(1, std::min(per_cu * cus, (int)NBMAX));
+      }
+      target = res;
+    }
     uint64_t tpb = 1;
     while (tpb * target < fg.ntiles) tpb <<= 1;
     fg.tpb = (uint32_t)tpb;
@@ -600,9 +647,9 @@ struct Circuit {
       ctx.pending_accumulate = 0;
       QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
                          mats, fg, ctx.slot_ptr(), (uint64_t)NBMAX * RED));
-      for (size_t k = 0; k < it.count; ++k) {
-        const Instr& in = ins[plan[it.first + k].instr];
-        if (is_var(in.kind)) ctx.commit(var_idx[plan[it.first + k].instr], grid);
+      for (uint32_t pi : it.ops) {
+        const Instr& in = ins[plan[pi].instr];
+        if (is_var(in.kind)) ctx.commit(var_idx[plan[pi].instr], grid);
       }
     }
     return nullptr;
@@ -662,7 +709,7 @@ struct Circuit {
         QDC_TRY(run_fused(item, pl, false, mats_off, {}));
         continue;
       }
-      const qdc_plan_op& op = pl[item.first];
+      const qdc_plan_op& op = pl[item.ops[0]];
       if (op.type == QDC_PLAN_REMAP) {
         QDC_TRY(remap(op, false));
         continue;
@@ -745,7 +792,7 @@ struct Circuit {
         QDC_TRY(run_fused(item, pl, have_bwd, mats_off, var_idx));
         continue;
       }
-      const qdc_plan_op& op = pl[item.first];
+      const qdc_plan_op& op = pl[item.ops[0]];
       if (op.type == QDC_PLAN_REMAP) {
         QDC_TRY(remap(op, have_bwd));
         continue;

@@ -548,8 +548,9 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
 // wave (~V shuffles for V values instead of 6V) and one LDS add per value into the wave's
 // accumulator slot for that gate; one partial per block and gate at the end.
 // ---------------------------------------------------------------------------------------
-constexpr int FMAX_OPS = 16;   // gates per fused pass
-constexpr int FMAX_ROWS = 5;   // far qubits per tile
+constexpr int FMAX_OPS = 32;   // gates per fused pass
+constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (LDS accumulators)
+constexpr int FMAX_ROWS = 8;   // far qubits per tile
 constexpr int FACC = 32;       // reals per gradient accumulator (16 complex)
 
 struct fop {
@@ -569,6 +570,71 @@ struct fgeo {
   uint32_t ngrad;  // gradient gates (their partials go to consecutive slots)
 };
 
+// Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the
+// natural (re, im) register pairs, with op_sel/neg modifiers doing the broadcast and swap:
+//   c += a.re * (f.re, f.im);   c += (-a.im * f.im, a.im * f.re)
+// Gate-matrix entries stay as one SGPR pair each ("s"): left to itself the compiler
+// materialises (a.re, a.re) and (-a.im, a.im) pairs — twice the SGPRs, which spill for a
+// two-qubit reverse step (A and B = 32 entries) and are re-read every iteration.
+#ifndef QDC_F64
+typedef float pk2 __attribute__((ext_vector_type(2)));
+// one instruction per asm statement, so the scheduler can interleave independent chains
+__device__ __forceinline__ pk2 pk_re_fma(pk2 a, pk2 f, pk2 c) {  // c + a.re * (f.re, f.im)
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(c) : "s"(a), "v"(f));
+  return c;
+}
+__device__ __forceinline__ pk2 pk_im_fma(pk2 a, pk2 f, pk2 c) {  // c + (-a.im f.im, a.im f.re)
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "+v"(c) : "s"(a), "v"(f));
+  return c;
+}
+__device__ __forceinline__ pk2 pk_re_mul(pk2 a, pk2 f) {  // a.re * (f.re, f.im)
+  pk2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "s"(a), "v"(f));
+  return r;
+}
+__device__ __forceinline__ pk2 vpk_re_fma(pk2 a, pk2 f, pk2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(c) : "v"(a), "v"(f));
+  return c;
+}
+__device__ __forceinline__ pk2 vpk_im_fma(pk2 a, pk2 f, pk2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "+v"(c) : "v"(a), "v"(f));
+  return c;
+}
+__device__ __forceinline__ cx ucfma(cx a, cx f, cx c) {  // c + a f, a wave-uniform
+  const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
+  return __builtin_bit_cast(cx, pk_im_fma(A, F, pk_re_fma(A, F, __builtin_bit_cast(pk2, c))));
+}
+__device__ __forceinline__ cx ucmul(cx a, cx f) {  // a f, a wave-uniform
+  const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
+  return __builtin_bit_cast(cx, pk_im_fma(A, F, pk_re_mul(A, F)));
+}
+__device__ __forceinline__ cx vcfma(cx a, cx f, cx c) {  // c + a f, both per lane
+  const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
+  return __builtin_bit_cast(cx, vpk_im_fma(A, F, vpk_re_fma(A, F, __builtin_bit_cast(pk2, c))));
+}
+#else
+__device__ __forceinline__ cx ucfma(cx a, cx f, cx c) { return cfma(a, f, c); }
+__device__ __forceinline__ cx ucmul(cx a, cx f) { return cmul(a, f); }
+__device__ __forceinline__ cx vcfma(cx a, cx f, cx c) { return cfma(a, f, c); }
+#endif
+
+// x <- M x with a wave-uniform M (row-major R x R)
+template <int R>
+__device__ __forceinline__ void umatvec(const cx* M, cx (&x)[R]) {
+  cx y[R];
+#pragma unroll
+  for (int p = 0; p < R; ++p) {
+    cx t = ucmul(M[p * R], x[0]);
+#pragma unroll
+    for (int q = 1; q < R; ++q) t = ucfma(M[p * R + q], x[q], t);
+    y[p] = t;
+  }
+#pragma unroll
+  for (int p = 0; p < R; ++p) x[p] = y[p];
+}
+
 // Lane select with a wave-uniform lane mask (v_cndmask): lanes set in `mask` take t.  Written
 // as asm because LLVM folds `upper ? x[h + i] : x[i]` on a register array into a dynamically
 // indexed array (a compare/select chain over every element: O(V^2) instructions).
@@ -587,18 +653,59 @@ __device__ __forceinline__ double lane_sel(double f, double t, uint64_t mask) {
   return __longlong_as_double((long long)(lo | (hi << 32)));
 }
 
-// Sum V reals over the 64 lanes; lanes whose low (6 - log2 V) index bits are zero end up
-// holding value idx(lane), and add it into acc[idx] (acc in LDS, one writer per index).
+// Cross-lane moves of one real (f64 as two dwords).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(v), CTRL,
+                                                               0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// (a, b) -> (a', b') with a' = [a.lo-half | b.lo-half], b' = [a.hi-half | b.hi-half], halves of
+// 32 lanes (W = 32, v_permlane32_swap) or alternating rows of 16 (W = 16, v_permlane16_swap)
+template <int W>
+__device__ __forceinline__ void half_swap(float& a, float& b) {
+  if constexpr (W == 32) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  } else {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  }
+}
+template <int W>
+__device__ __forceinline__ void half_swap(double& a, double& b) {
+  const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+  float alo = __uint_as_float((uint32_t)ua), ahi = __uint_as_float((uint32_t)(ua >> 32));
+  float blo = __uint_as_float((uint32_t)ub), bhi = __uint_as_float((uint32_t)(ub >> 32));
+  half_swap<W>(alo, blo);
+  half_swap<W>(ahi, bhi);
+  a = __longlong_as_double((long long)(((uint64_t)__float_as_uint(ahi) << 32) | __float_as_uint(alo)));
+  b = __longlong_as_double((long long)(((uint64_t)__float_as_uint(bhi) << 32) | __float_as_uint(blo)));
+}
+
+// Sum V reals over the 64 lanes (reduce-scatter): afterwards value idx(lane) sits in the lanes
+// whose low (6 - log2 V) index bits are zero, and is added into acc[idx] (acc in LDS, one
+// writer per index).  Offsets 32 and 16 are one v_permlane{32,16}_swap + one add per value
+// pair; offsets 8, 4, 2, 1 are DPP moves (row_ror:8, row_half_mirror, quad_perm) with lane
+// selects.  Partner lanes always agree on the bits above the current offset, so they hold the
+// same index set; the lane with the offset bit set keeps the upper half.
 template <int V>
 __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
-  // lanes with bit o of the lane id set, o = 32, 16, ..., 1
   constexpr uint64_t UPPER[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull,
                                  0xFF00FF00FF00FF00ull, 0xF0F0F0F0F0F0F0F0ull,
                                  0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};
+  constexpr int CTRL[6] = {0, 0, 0x128 /*row_ror:8*/, 0x141 /*row_half_mirror*/,
+                           0x4E /*quad_perm 2,3,0,1*/, 0xB1 /*quad_perm 1,0,3,2*/};
   const int lane = threadIdx.x & 63;
   int idx = 0;
-  // reduce-scatter steps: offsets 32, 16, ... while more than one value remains; the upper
-  // half of each lane pair keeps values [half, len), the lower half keeps [0, half)
 #pragma unroll
   for (int step = 0; step < 6; ++step) {
     const int o = 32 >> step;
@@ -607,13 +714,40 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
       const int half = len >> 1;
 #pragma unroll
       for (int i = 0; i < half; ++i) {
-        const real mine = lane_sel(x[i], x[half + i], UPPER[step]);
-        const real send = lane_sel(x[half + i], x[i], UPPER[step]);
-        x[i] = mine + __shfl_xor(send, o, 64);
+        if (step == 0) {
+          half_swap<32>(x[i], x[half + i]);
+          x[i] += x[half + i];
+        } else if (step == 1) {
+          half_swap<16>(x[i], x[half + i]);
+          x[i] += x[half + i];
+        } else {
+          const real mine = lane_sel(x[i], x[half + i], UPPER[step]);
+          const real send = lane_sel(x[half + i], x[i], UPPER[step]);
+          if (step == 2) x[i] = mine + dpp_mov<CTRL[2]>(send);
+          if (step == 3) x[i] = mine + dpp_mov<CTRL[3]>(send);
+          if (step == 4) x[i] = mine + dpp_mov<CTRL[4]>(send);
+          if (step == 5) x[i] = mine + dpp_mov<CTRL[5]>(send);
+        }
       }
       idx += (lane & o) ? half : 0;
     } else {
-      x[0] += __shfl_xor(x[0], o, 64);
+      if (step == 0) {
+        real y = x[0];
+        half_swap<32>(x[0], y);
+        x[0] += y;
+      } else if (step == 1) {
+        real y = x[0];
+        half_swap<16>(x[0], y);
+        x[0] += y;
+      } else if (step == 2) {
+        x[0] += dpp_mov<CTRL[2]>(x[0]);
+      } else if (step == 3) {
+        x[0] += dpp_mov<CTRL[3]>(x[0]);
+      } else if (step == 4) {
+        x[0] += dpp_mov<CTRL[4]>(x[0]);
+      } else {
+        x[0] += dpp_mov<CTRL[5]>(x[0]);
+      }
     }
   }
   const int spread = 64 / V;  // lanes holding the same idx
@@ -621,45 +755,82 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
 }
 
 template <bool TWO, int TB>
-__global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* __restrict__ b,
+#ifndef QDC_FUSED_WAVES
+#define QDC_FUSED_WAVES 4  // waves/SIMD the fused kernels are register-allocated for
+#endif
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED_WAVES))) void k_fused(chunk* __restrict__ f, chunk* __restrict__ b,
                                                  const fop* __restrict__ ops,
                                                  const cx* __restrict__ mats, fgeo fg,
                                                  cx* __restrict__ partials,
                                                  uint64_t slot_stride) {
   constexpr int NS = TWO ? 2 : 1;
+  constexpr int CPT = TB / BLOCK;  // chunks of each state per thread and tile
+  static_assert(TB % BLOCK == 0 && TB * VEC >= 4 * BLOCK, "tile must cover the block");
   __shared__ chunk lds[NS][TB];
-  __shared__ real accw[BLOCK / 64][FMAX_OPS][FACC];
+  __shared__ real accw[TWO ? BLOCK / 64 : 1][FMAX_GRAD][FACC];
   const uint32_t t = threadIdx.x;
   const int wave = t >> 6;
   if constexpr (TWO) {
-    for (uint32_t i = t; i < (BLOCK / 64) * FMAX_OPS * FACC; i += BLOCK)
+    for (uint32_t i = t; i < (BLOCK / 64) * FMAX_GRAD * FACC; i += BLOCK)
       (&accw[0][0][0])[i] = 0;
   }
-  const uint32_t tc = 1u << (fg.lc + fg.h);  // chunks per tile (== TB except tiny states)
-  const uint32_t ta = tc * VEC;              // amplitudes per tile
+  // a tile is always TB chunks (lc + h == log2 TB; the host fuses nothing in smaller states),
+  // so no per-chunk guards: divergent guards make the waitcnt pass drain every prefetch
+  constexpr uint32_t ta = TB * VEC;  // amplitudes per tile
   cx* lf = reinterpret_cast<cx*>(&lds[0][0]);
   cx* lb = reinterpret_cast<cx*>(&lds[NS - 1][0]);
-  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
-  for (uint32_t tt = 0; tt < fg.tpb; ++tt) {
-    const uint64_t tile = tile0 + tt;
-    if (tile >= fg.ntiles) break;
+  // thread-owned tile chunks c = t + i*BLOCK sit at the same offset from every tile's base
+  uint64_t off[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const uint32_t c = t + (uint32_t)i * BLOCK;
+    uint64_t o = c & ((1u << fg.lc) - 1u);
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) o += (uint64_t)((c >> (fg.lc + k)) & 1u) << fg.hb[k];
+    off[i] = o;
+  }
+  auto tile_base = [&](uint64_t tile) {
     uint64_t base = tile << fg.lc;
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    auto gidx = [&](uint32_t c) {
-      uint64_t gi = base + (c & ((1u << fg.lc) - 1u));
+    return base;
+  };
+  // software pipeline: the next tile's chunks are in flight while this tile's gates run
+  chunk pf[NS][CPT];
+  auto prefetch = [&](uint64_t base) {
 #pragma unroll
-      for (int k = 0; k < FMAX_ROWS; ++k)
-        if ((uint32_t)k < fg.h) gi += (uint64_t)((c >> (fg.lc + k)) & 1u) << fg.hb[k];
-      return gi;
-    };
-    for (uint32_t c = t; c < tc; c += BLOCK) {
-      const uint64_t gi = gidx(c);
-      lds[0][c] = ldc(f + gi);
-      if constexpr (TWO) lds[1][c] = ldc(b + gi);
+    for (int i = 0; i < CPT; ++i) {
+      pf[0][i] = ldc(f + base + off[i]);
+      if constexpr (TWO) pf[NS - 1][i] = ldc(b + base + off[i]);
     }
+  };
+  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
+  const uint32_t count =
+      tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+  auto fill = [&]() {  // pf -> LDS, each thread its own chunks
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const uint32_t c = t + (uint32_t)i * BLOCK;
+      lds[0][c] = pf[0][i];
+      if constexpr (TWO) lds[NS - 1][c] = pf[NS - 1][i];
+    }
+  };
+  uint64_t base = count ? tile_base(tile0) : 0;
+  if (count) {
+    prefetch(base);
+    fill();
+  }
+  // loop rotated so the LDS refill waits (vmcnt) sit after this tile's stores in straight-line
+  // code: they wait for the prefetched loads only, not for the stores issued after them
+  for (uint32_t tt = 0; tt < count; ++tt) {
     __syncthreads();
+    const uint64_t cur = base;
+    if (tt + 1 < count) {
+      base = tile_base(tile0 + tt + 1);
+      prefetch(base);
+    }
     uint32_t gi_op = 0;
     for (uint32_t j = 0; j < fg.nops; ++j) {
       const fop op = ops[j];
@@ -667,28 +838,31 @@ __global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* _
       const bool grad = TWO && (op.kind & 4u);
       const cx* M = mats + op.mat;
       if (kind == 0) {  // one-qubit dense
-        mat<2> A, B;
+        cx A[4], B[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) A.a[i] = M[i];
+        for (int i = 0; i < 4; ++i) A[i] = M[i];
         if constexpr (TWO) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) B.a[i] = M[4 + i];
+          for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
         }
         cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         const uint32_t s1 = 1u << op.t1;
-        for (uint32_t grp = t; grp < ta / 2; grp += BLOCK) {
+        for (uint32_t it = 0; it < ta / (2 * BLOCK); ++it) {
+          const uint32_t grp = t + it * BLOCK;
           const uint32_t a0 = (uint32_t)insert_zero(grp, op.t1);
           cx fx[2] = {lf[a0], lf[a0 + s1]};
+          umatvec<2>(A, fx);
           if constexpr (TWO) {
             cx bx[2] = {lb[a0], lb[a0 + s1]};
-            if (grad)
-              op_vector<OP_REVERSE_GRAD, 2>(A, B, fx, bx, acc);
-            else
-              op_vector<OP_REVERSE, 2>(A, B, fx, bx, acc);
+            if (grad) {
+#pragma unroll
+              for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) acc[p * 2 + q] = vcfma(bx[p], fx[q], acc[p * 2 + q]);
+            }
+            umatvec<2>(B, bx);
             lb[a0] = bx[0];
             lb[a0 + s1] = bx[1];
-          } else {
-            matvec<2>(A, fx);
           }
           lf[a0] = fx[0];
           lf[a0 + s1] = fx[1];
@@ -703,12 +877,12 @@ __global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* _
           wave_reduce_add<8>(v, &accw[wave][gi_op][0]);
         }
       } else if (kind == 1) {  // two-qubit dense
-        mat<4> A, B;
+        cx A[16], B[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) A.a[i] = M[i];
+        for (int i = 0; i < 16; ++i) A[i] = M[i];
         if constexpr (TWO) {
 #pragma unroll
-          for (int i = 0; i < 16; ++i) B.a[i] = M[16 + i];
+          for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
         }
         cx acc[16];
 #pragma unroll
@@ -716,23 +890,26 @@ __global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* _
         const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
         const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
-        for (uint32_t grp = t; grp < ta / 4; grp += BLOCK) {
+        for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
+          const uint32_t grp = t + it * BLOCK;
           const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
           const uint32_t off[4] = {0, s1, s2, s1 + s2};
           cx fx[4], bx[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) fx[r] = lf[a0 + off[r]];
+          umatvec<4>(A, fx);
           if constexpr (TWO) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bx[r] = lb[a0 + off[r]];
-            if (grad)
-              op_vector<OP_REVERSE_GRAD, 4>(A, B, fx, bx, acc);
-            else
-              op_vector<OP_REVERSE, 4>(A, B, fx, bx, acc);
+            if (grad) {
+#pragma unroll
+              for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[p * 4 + q] = vcfma(bx[p], fx[q], acc[p * 4 + q]);
+            }
+            umatvec<4>(B, bx);
 #pragma unroll
             for (int r = 0; r < 4; ++r) lb[a0 + off[r]] = bx[r];
-          } else {
-            matvec<4>(A, fx);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) lf[a0 + off[r]] = fx[r];
@@ -759,17 +936,18 @@ __global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* _
         const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
         const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
-        for (uint32_t grp = t; grp < ta / 4; grp += BLOCK) {
+        for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
+          const uint32_t grp = t + it * BLOCK;
           const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
           const uint32_t off[4] = {0, s1, s2, s1 + s2};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const cx fv = cmul(A[r], lf[a0 + off[r]]);
+            const cx fv = ucmul(A[r], lf[a0 + off[r]]);
             lf[a0 + off[r]] = fv;
             if constexpr (TWO) {
               const cx bv = lb[a0 + off[r]];
-              if (grad) acc[r] = cfma(bv, fv, acc[r]);
-              lb[a0 + off[r]] = cmul(B[r], bv);
+              if (grad) acc[r] = vcfma(bv, fv, acc[r]);
+              lb[a0 + off[r]] = ucmul(B[r], bv);
             }
           }
         }
@@ -786,12 +964,14 @@ __global__ __launch_bounds__(BLOCK) void k_fused(chunk* __restrict__ f, chunk* _
       gi_op += grad ? 1u : 0u;
       __syncthreads();
     }
-    for (uint32_t c = t; c < tc; c += BLOCK) {
-      const uint64_t gi = gidx(c);
-      stc(f + gi, lds[0][c]);
-      if constexpr (TWO) stc(b + gi, lds[1][c]);
+    // each thread stores (and next refills) only its own chunks: no barrier needed here
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const uint32_t c = t + (uint32_t)i * BLOCK;
+      stc(f + cur + off[i], lds[0][c]);
+      if constexpr (TWO) stc(b + cur + off[i], lds[NS - 1][c]);
     }
-    __syncthreads();  // the next tile overwrites lds
+    if (tt + 1 < count) fill();
   }
   if constexpr (TWO) {
     // one partial (16 complex) per block and gradient gate: slot k at partials + k*slot_stride

@@ -115,7 +115,9 @@ _LIBS: dict = {}
 
 
 def lib_path(precision: str) -> Path:
-    return LIB_DIR / f"libqdc_{precision}.so"
+    """In-tree build; QDC_LIB_DIR selects another build of the same library (experiments)."""
+    d = Path(os.environ["QDC_LIB_DIR"]) if os.environ.get("QDC_LIB_DIR") else LIB_DIR
+    return d / f"libqdc_{precision}.so"
 
 
 def load(precision: str = "f32"):
