@@ -17,6 +17,7 @@
 #include "qdc/circuit.h"
 #include "qdc_device.hpp"
 #include "qdc_shard.hpp"
+#include "qdc_stage.hpp"
 
 namespace qdc {
 
@@ -177,11 +178,12 @@ struct Circuit {
   // fused multi-gate passes
   int fuse = 1;             // 0: one HBM pass per gate
   uint32_t fuse_max_ops = FMAX_OPS;
-  uint32_t fuse_lcmin = LOWBITS;  // min contiguous chunk bits of a fused tile
+  uint32_t fuse_lcmin = 3;  // min contiguous chunk bits of a fused tile (128-B rows)
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   uint32_t fused_resident[2] = {0, 0};
   unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
   unsigned char* prog_host = nullptr;  // pinned staging
+  std::vector<StagePost> stage_post;   // gradient recipes of the last backward's stages
   size_t prog_cap = 0;
 
   // world = total shards (power of two), nlocal = shards in this process
@@ -403,7 +405,9 @@ struct Circuit {
     std::vector<uint32_t> ops;   // plan indices (one for type 0/1), program order
     uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {};
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
+    uint32_t nstage = 0;  // fop count (stages) of the pass
     uint32_t ngrad = 0;
+    std::vector<uint32_t> grad_slots;  // gradient-buffer slot of each gradient stage
   };
   static constexpr uint32_t TILE_CHUNKS_1 = 2048;  // one-state fused tile (chunks)
   static constexpr uint32_t TILE_CHUNKS_2 = 1024;  // two-state fused tile (chunks per state)
@@ -502,21 +506,53 @@ struct Circuit {
     return items;
   }
 
-  // Lay out every fused group's fop array and matrices in one pinned buffer, then upload it.
-  // backward: `first_inject` = plan index of the first cotangent injection (groups before it
-  // only uncompute fwd).
+  // Split a pass (plan indices in pass order) into stages: greedy in program order, a gate
+  // joins the current stage if none of its qubits is blocked (an earlier gate on it is left
+  // for a later stage) and the stage stays within two qubits.  Per qubit, order is kept.
+  std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
+                                                     const std::vector<qdc_plan_op>& plan) const {
+    std::vector<std::vector<uint32_t>> stages;
+    std::vector<uint32_t> rem = pass;
+    while (!rem.empty()) {
+      std::vector<uint32_t> st, rest;
+      uint64_t q = 0, blocked = 0;
+      for (uint32_t k : rem) {
+        const qdc_plan_op& g = plan[k];
+        const uint64_t gq = (1ull << g.pos2) | (1ull << g.pos1);
+        if ((gq & blocked) || __builtin_popcountll(q | gq) > 2) {
+          blocked |= gq;
+          rest.push_back(k);
+          continue;
+        }
+        st.push_back(k);
+        q |= gq;
+      }
+      stages.push_back(std::move(st));
+      rem.swap(rest);
+    }
+    return stages;
+  }
+
+  // Lay out every fused pass's stage descriptors and stage matrices (A = product of the
+  // applied matrices, B = product of the bwd pull-backs) in one pinned buffer, then upload it.
+  // backward: `first_inject` = plan index of the first cotangent injection (passes before it
+  // only uncompute fwd); gradient stages get slots nvar, nvar+1, ... of the gradient buffer and
+  // a recipe in stage_post (qdc_stage.hpp).
   const char* build_program(std::vector<Item>& items, const std::vector<qdc_plan_op>& plan,
                             bool backward, size_t first_inject, const Flat& cg, const Flat& vg,
-                            const std::vector<size_t>& gidx, size_t& mats_off) {
-    size_t nops = 0, nmat = 0;
-    for (auto& it : items)
-      if (it.type == 2) {
-        nops += it.ops.size();
-        nmat += it.ops.size() * 32;
+                            const std::vector<size_t>& gidx, size_t& mats_off,
+                            const std::vector<uint32_t>& var_idx, uint32_t nvar) {
+    stage_post.clear();
+    std::vector<std::vector<std::vector<uint32_t>>> stages_of(items.size());
+    size_t nops = 0;
+    for (size_t ii = 0; ii < items.size(); ++ii)
+      if (items[ii].type == 2) {
+        stages_of[ii] = stage_partition(items[ii].ops, plan);
+        nops += stages_of[ii].size();
       }
     if (nops == 0) return nullptr;
     mats_off = ((nops * sizeof(fop) + 255) / 256) * 256;
-    const size_t bytes = mats_off + nmat * sizeof(cx);
+    const size_t bytes = mats_off + nops * 32 * sizeof(cx);
     if (bytes > prog_cap) {
       QDC_HIP(hipStreamSynchronize(ctx.stream));
       if (prog_dev) QDC_HIP(hipFree(prog_dev));
@@ -529,62 +565,115 @@ struct Circuit {
     fop* fops = reinterpret_cast<fop*>(prog_host);
     cx* mats = reinterpret_cast<cx*>(prog_host + mats_off);
     size_t fo = 0, mo = 0;
-    for (auto& it : items) {
+    uint32_t next_slot = nvar;
+    for (size_t ii = 0; ii < items.size(); ++ii) {
+      Item& it = items[ii];
       if (it.type != 2) continue;
       it.fop_off = fo * sizeof(fop);
+      it.grad_slots.clear();
       const bool two = backward && it.ops[0] > first_inject;
-      for (uint32_t pi : it.ops) {
-        const qdc_plan_op& op = plan[pi];
-        const Instr& in = ins[op.instr];
-        const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
-        auto local_bit = [&](uint32_t p) -> uint32_t {
-          if (p < (uint32_t)LV + it.lc) return p;
-          for (uint32_t r = 0; r < it.h; ++r)
-            if (it.hb[r] == p - LV) return LV + it.lc + r;
-          return 0xffffffffu;  // unreachable: tile_config covered every bit
-        };
+      auto local_bit = [&](uint32_t p) -> uint32_t {
+        if (p < (uint32_t)LV + it.lc) return p;
+        for (uint32_t r = 0; r < it.h; ++r)
+          if (it.hb[r] == p - LV) return LV + it.lc + r;
+        return 0xffffffffu;  // unreachable: tile_config covered every bit
+      };
+      for (const auto& st : stages_of[ii]) {
+        // stage qubits (physical positions), lo < hi
+        uint64_t qm = 0;
+        bool all_diag = true, any_grad = false;
+        for (uint32_t pi : st) {
+          qm |= (1ull << plan[pi].pos2) | (1ull << plan[pi].pos1);
+          all_diag = all_diag && is_diag(ins[plan[pi].instr].kind);
+          any_grad = any_grad || (two && is_var(ins[plan[pi].instr].kind));
+        }
+        const uint32_t lo = (uint32_t)__builtin_ctzll(qm);
+        const uint32_t hi = 63u - (uint32_t)__builtin_clzll(qm);
+        const int R = lo == hi ? 2 : 4;
+        SMat A = smat_identity(R), B = smat_identity(R);
+        StagePost post;
+        post.R = R;
+        post.diag_only = all_diag;
+        for (uint32_t pi : st) {
+          const qdc_plan_op& op = plan[pi];
+          const Instr& in = ins[op.instr];
+          const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
+          const bool dg = is_diag(in.kind);
+          int role;
+          if (R == 2)
+            role = ROLE_Q1_ONLY;
+          else if (is_q1_gate(in.kind))
+            role = op.pos2 == lo ? ROLE_Q1_LO : ROLE_Q1_HI;
+          else
+            role = op.pos2 == hi ? ROLE_Q2 : ROLE_Q2_SWAP;
+          // the applied matrix a (forward: U; uncompute: U^dagger / U^-1 / conj diagonal) and
+          // the pull-back b = U^T (diagonal: d), each in the gate's own basis
+          cd ga[16], gb[16];
+          if (dg) {
+            const diag4 d = to_diag(g4);
+            const diag4 a = backward ? conj_diag(d) : d;
+            for (int i = 0; i < 4; ++i) {
+              ga[i] = cd(a.a[i].x, a.a[i].y);
+              gb[i] = cd(d.a[i].x, d.a[i].y);
+            }
+          } else if (is_q1_gate(in.kind)) {
+            const mat<2> u = to_mat<2>(g4);
+            mat<2> a = u;
+            if (backward) {
+              if (is_nonu(in.kind))
+                QDC_TRY(inverse<2>(u, a));
+              else
+                a = conj_transpose<2>(u);
+            }
+            const mat<2> bt = transpose<2>(u);
+            for (int i = 0; i < 4; ++i) {
+              ga[i] = cd(a.a[i].x, a.a[i].y);
+              gb[i] = cd(bt.a[i].x, bt.a[i].y);
+            }
+          } else {
+            const mat<4> u = to_mat<4>(g4);
+            mat<4> a = u;
+            if (backward) {
+              if (is_nonu(in.kind))
+                QDC_TRY(inverse<4>(u, a));
+              else
+                a = conj_transpose<4>(u);
+            }
+            const mat<4> bt = transpose<4>(u);
+            for (int i = 0; i < 16; ++i) {
+              ga[i] = cd(a.a[i].x, a.a[i].y);
+              gb[i] = cd(bt.a[i].x, bt.a[i].y);
+            }
+          }
+          const SMat Ea = stage_embed(ga, dg, role, R), Eb = stage_embed(gb, dg, role, R);
+          const SMat Anew = smat_mul(Ea, A);
+          if (two && is_var(in.kind))
+            post.gates.push_back(StageGate{var_idx[op.instr], dg, role, B, smat_transpose(Anew)});
+          A = Anew;
+          B = smat_mul(Eb, B);
+        }
         fop& F = fops[fo++];
-        F.t2 = local_bit(op.pos2);
-        F.t1 = local_bit(op.pos1);
+        F.t1 = local_bit(lo);
+        F.t2 = local_bit(hi);
         F.mat = (uint32_t)mo;
-        const bool grad = two && is_var(in.kind);
-        if (is_diag(in.kind)) {
-          F.kind = 2 | (grad ? 4u : 0u);
-          const diag4 d = to_diag(g4);
-          const diag4 a = backward ? conj_diag(d) : d;
-          for (int i = 0; i < 4; ++i) mats[mo + i] = a.a[i];
-          for (int i = 0; i < 4; ++i) mats[mo + 4 + i] = d.a[i];
-          mo += 8;
-        } else if (is_q1_gate(in.kind)) {
-          F.kind = 0 | (grad ? 4u : 0u);
-          const mat<2> u = to_mat<2>(g4);
-          mat<2> a = u;
-          if (backward) {
-            if (is_nonu(in.kind))
-              QDC_TRY(inverse<2>(u, a));
-            else
-              a = conj_transpose<2>(u);
-          }
-          const mat<2> bt = transpose<2>(u);
-          for (int i = 0; i < 4; ++i) mats[mo + i] = a.a[i];
-          for (int i = 0; i < 4; ++i) mats[mo + 4 + i] = bt.a[i];
-          mo += 8;
-        } else {
-          F.kind = 1 | (grad ? 4u : 0u);
-          const mat<4> u = to_mat<4>(g4);
-          mat<4> a = u;
-          if (backward) {
-            if (is_nonu(in.kind))
-              QDC_TRY(inverse<4>(u, a));
-            else
-              a = conj_transpose<4>(u);
-          }
-          const mat<4> bt = transpose<4>(u);
-          for (int i = 0; i < 16; ++i) mats[mo + i] = a.a[i];
-          for (int i = 0; i < 16; ++i) mats[mo + 16 + i] = bt.a[i];
-          mo += 32;
+        const uint32_t kind = all_diag ? 2u : (R == 2 ? 0u : 1u);
+        F.kind = kind | (any_grad ? 4u : 0u);
+        const int n = all_diag ? 4 : R * R;
+        for (int i = 0; i < n; ++i) {
+          const cd va = all_diag ? A.a[i * 4 + i] : A.a[i];
+          const cd vb = all_diag ? B.a[i * 4 + i] : B.a[i];
+          mats[mo + i] = cx{(real)va.real(), (real)va.imag()};
+          mats[mo + n + i] = cx{(real)vb.real(), (real)vb.imag()};
+        }
+        mo += 2 * n;
+        if (any_grad) {
+          post.slot = next_slot++;
+          it.grad_slots.push_back(post.slot);
+          stage_post.push_back(std::move(post));
         }
       }
+      it.ngrad = (uint32_t)it.grad_slots.size();
+      it.nstage = (uint32_t)stages_of[ii].size();
     }
     QDC_HIP(hipMemcpyAsync(prog_dev, prog_host, mats_off + mo * sizeof(cx),
                            hipMemcpyHostToDevice, ctx.stream));
@@ -594,12 +683,12 @@ struct Circuit {
   // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
   // gradient gates write partials for gradient buffer rows var_idx[...].
   const char* run_fused(const Item& it, const std::vector<qdc_plan_op>& plan, bool two,
-                        size_t mats_off, const std::vector<uint32_t>& var_idx) {
+                        size_t mats_off) {
     fgeo fg{};
     fg.lc = it.lc;
     fg.h = it.h;
     for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];
-    fg.nops = (uint32_t)it.ops.size();
+    fg.nops = it.nstage;
     fg.ngrad = two ? it.ngrad : 0;
     fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
     // one wave of resident blocks, each pipelining a contiguous run of tiles
@@ -647,10 +736,7 @@ struct Circuit {
       ctx.pending_accumulate = 0;
       QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
                          mats, fg, ctx.slot_ptr(), (uint64_t)NBMAX * RED));
-      for (uint32_t pi : it.ops) {
-        const Instr& in = ins[plan[pi].instr];
-        if (is_var(in.kind)) ctx.commit(var_idx[plan[pi].instr], grid);
-      }
+      for (uint32_t slot : it.grad_slots) ctx.commit(slot, grid);
     }
     return nullptr;
   }
@@ -703,10 +789,10 @@ struct Circuit {
     const std::vector<qdc_plan_op> pl = plan(mode);
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
-    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off));
+    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0));
     for (const Item& item : items) {
       if (item.type == 2) {
-        QDC_TRY(run_fused(item, pl, false, mats_off, {}));
+        QDC_TRY(run_fused(item, pl, false, mats_off));
         continue;
       }
       const qdc_plan_op& op = pl[item.ops[0]];
@@ -737,14 +823,18 @@ struct Circuit {
     return collect(sh[0].dens, widths, out);
   }
 
-  const char* collect(const cx* dev, const std::vector<int>& widths, qdc_complex* out) {
+  // D2H of `total` (>= widths.size()) result slots into host_out; the first widths.size()
+  // are unpacked into `out`.
+  const char* collect(const cx* dev, const std::vector<int>& widths, qdc_complex* out,
+                      size_t total = 0) {
     const size_t count = widths.size();
-    if (count == 0) {
+    total = std::max(total, count);
+    if (total == 0) {
       QDC_HIP(hipStreamSynchronize(ctx.stream));
       return nullptr;
     }
-    QDC_TRY(ensure_host(count * RED));
-    QDC_HIP(hipMemcpyAsync(host_out, dev, sizeof(cx) * count * RED, hipMemcpyDeviceToHost,
+    QDC_TRY(ensure_host(total * RED));
+    QDC_HIP(hipMemcpyAsync(host_out, dev, sizeof(cx) * total * RED, hipMemcpyDeviceToHost,
                            ctx.stream));
     QDC_HIP(hipStreamSynchronize(ctx.stream));
     size_t w = 0;
@@ -765,11 +855,12 @@ struct Circuit {
     const size_t nvar = n_var();
     for (auto& s : sh)
       if (!s.bwd) QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
-    QDC_TRY(ensure_out(false, std::max<size_t>(nvar, 1) * RED));
+    // slots [0, nvar): per-gate gradients; [nvar, nvar + stages): fused stages' Gamma
+    const size_t nslots = std::max<size_t>(2 * nvar, 1);
+    QDC_TRY(ensure_out(false, nslots * RED));
     // variable gates met before the first cotangent keep zero gradients (circuit.rs:327-331)
     for (auto& s : sh)
-      QDC_HIP(hipMemsetAsync(s.grads, 0, sizeof(cx) * std::max<size_t>(nvar, 1) * RED,
-                             ctx.stream));
+      QDC_HIP(hipMemsetAsync(s.grads, 0, sizeof(cx) * nslots * RED, ctx.stream));
     std::vector<uint32_t> var_idx(ins.size(), 0);
     {
       uint32_t v = 0;
@@ -786,10 +877,11 @@ struct Circuit {
       }
     std::vector<Item> items = fuse_items(pl, true);
     size_t mats_off = 0;
-    QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off));
+    QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
+                          (uint32_t)nvar));
     for (const Item& item : items) {
       if (item.type == 2) {
-        QDC_TRY(run_fused(item, pl, have_bwd, mats_off, var_idx));
+        QDC_TRY(run_fused(item, pl, have_bwd, mats_off));
         continue;
       }
       const qdc_plan_op& op = pl[item.ops[0]];
@@ -844,13 +936,40 @@ struct Circuit {
       }
     }
     QDC_TRY(ctx.flush());
+    const size_t used = nvar + stage_post.size();
     std::vector<cx*> bufs;
     for (auto& s : sh) bufs.push_back(s.grads);
-    QDC_TRY(ex.allreduce(ctx, bufs, nvar * RED));
+    QDC_TRY(ex.allreduce(ctx, bufs, used * RED));
     std::vector<int> widths;
     for (auto& in : ins)
       if (is_var(in.kind)) widths.push_back(gate_len(in.kind));
-    return collect(sh[0].grads, widths, out);
+    QDC_TRY(collect(sh[0].grads, widths, out, used));
+    // gradients of fused stages: G = ptrace(L Gamma Rt) per gate (qdc_stage.hpp)
+    if (!stage_post.empty()) {
+      std::vector<size_t> off(widths.size() + 1, 0);
+      for (size_t j = 0; j < widths.size(); ++j) off[j + 1] = off[j] + widths[j];
+      for (const StagePost& st : stage_post) {
+        SMat G = smat_identity(st.R);
+        const cx* g = host_out + (size_t)st.slot * RED;
+        if (st.diag_only) {
+          for (int i = 0; i < 16; ++i) G.a[i] = 0;
+          for (int r = 0; r < 4; ++r) G.a[r * 4 + r] = cd(g[r].x, g[r].y);
+        } else {
+          for (int i = 0; i < st.R * st.R; ++i) G.a[i] = cd(g[i].x, g[i].y);
+        }
+        for (const StageGate& sg : st.gates) {
+          const SMat M = smat_mul(smat_mul(sg.L, G), sg.Rt);
+          cd v[16];
+          stage_extract(M, sg.diag, sg.role, v);
+          qdc_complex* o = out + off[sg.var];
+          for (int k = 0; k < widths[sg.var]; ++k) {
+            o[k].re = (qdc_real)v[k].real();
+            o[k].im = (qdc_real)v[k].imag();
+          }
+        }
+      }
+    }
+    return nullptr;
   }
 };
 

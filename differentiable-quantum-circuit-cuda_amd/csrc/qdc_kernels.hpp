@@ -538,18 +538,19 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
 
 
 // ---------------------------------------------------------------------------------------
-// FUSED family: a run of consecutive gates whose qubits all fit one
-// tile is applied in ONE HBM pass.  A tile = TB chunks of each state: `lc` contiguous low
-// chunk bits (>= 6: every wave instruction stays on a contiguous KiB) plus `h` row bits at
-// far chunk positions hb[].  The gates run one after the other on LDS (a barrier between
-// gates); a two-state (reverse) program uncomputes fwd, accumulates each variable gate's
-// gradient and pulls bwd back, exactly as k_direct / k_tile do for one gate.
-// Gradients: per thread in registers during a gate, then a reduce-scatter butterfly over the
-// wave (~V shuffles for V values instead of 6V) and one LDS add per value into the wave's
-// accumulator slot for that gate; one partial per block and gate at the end.
+// FUSED family: a pass of gates whose qubits all fit one tile is
+// applied in ONE HBM pass.  A tile = TB chunks of each state: `lc` contiguous low chunk bits
+// (>= 3: 128-B rows) plus `h` row bits at far chunk positions hb[].  The pass runs its ops on
+// LDS with a barrier between ops; each op is a register STAGE (qdc_stage.hpp): a run of gates
+// within one qubit pair, applied as the host-formed products A (fwd) and B (bwd pull-back).  A
+// two-state (reverse) program also accumulates the stage's Gamma = sum b0 f0^T of the
+// stage-entry states, from which the host derives every gate's gradient exactly.
+// Gamma: per thread in registers during an op, then a reduce-scatter over the wave
+// (permlane swaps + DPP, ~V instructions for V values) and one LDS add per value into the
+// wave's accumulator slot; one partial per block and gradient stage at the end.
 // ---------------------------------------------------------------------------------------
-constexpr int FMAX_OPS = 32;   // gates per fused pass
-constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (LDS accumulators)
+constexpr int FMAX_OPS = 32;   // gates per fused pass (>= its stages)
+constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (>= its gradient stages)
 constexpr int FMAX_ROWS = 8;   // far qubits per tile
 constexpr int FACC = 32;       // reals per gradient accumulator (16 complex)
 
@@ -851,18 +852,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           const uint32_t grp = t + it * BLOCK;
           const uint32_t a0 = (uint32_t)insert_zero(grp, op.t1);
           cx fx[2] = {lf[a0], lf[a0 + s1]};
-          umatvec<2>(A, fx);
           if constexpr (TWO) {
             cx bx[2] = {lb[a0], lb[a0 + s1]};
-            if (grad) {
+            if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int q = 0; q < 2; ++q) acc[p * 2 + q] = vcfma(bx[p], fx[q], acc[p * 2 + q]);
             }
+            umatvec<2>(A, fx);
             umatvec<2>(B, bx);
             lb[a0] = bx[0];
             lb[a0 + s1] = bx[1];
+          } else {
+            umatvec<2>(A, fx);
           }
           lf[a0] = fx[0];
           lf[a0 + s1] = fx[1];
@@ -897,19 +900,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           cx fx[4], bx[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) fx[r] = lf[a0 + off[r]];
-          umatvec<4>(A, fx);
           if constexpr (TWO) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bx[r] = lb[a0 + off[r]];
-            if (grad) {
+            if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 4; ++p)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc[p * 4 + q] = vcfma(bx[p], fx[q], acc[p * 4 + q]);
             }
+            umatvec<4>(A, fx);
             umatvec<4>(B, bx);
 #pragma unroll
             for (int r = 0; r < 4; ++r) lb[a0 + off[r]] = bx[r];
+          } else {
+            umatvec<4>(A, fx);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) lf[a0 + off[r]] = fx[r];
@@ -942,11 +947,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           const uint32_t off[4] = {0, s1, s2, s1 + s2};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const cx fv = ucmul(A[r], lf[a0 + off[r]]);
-            lf[a0 + off[r]] = fv;
+            const cx f0 = lf[a0 + off[r]];
+            lf[a0 + off[r]] = ucmul(A[r], f0);
             if constexpr (TWO) {
               const cx bv = lb[a0 + off[r]];
-              if (grad) acc[r] = vcfma(bv, fv, acc[r]);
+              if (grad) acc[r] = vcfma(bv, f0, acc[r]);
               lb[a0 + off[r]] = ucmul(B[r], bv);
             }
           }

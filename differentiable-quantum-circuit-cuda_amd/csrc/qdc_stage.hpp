@@ -1,0 +1,154 @@
+// qdc_stage.hpp — host algebra of the fused passes' register stages.
+//
+// A fused pass is split into stages: runs of gates (per-qubit program order kept) whose
+// qubits all lie in one pair {lo, hi} of tile bits (or one bit).  The kernel treats a stage as
+// one virtual gate: it applies the stage products A = A_m ... A_1 and B = B_m ... B_1 and, for
+// the reverse sweep, accumulates ONE outer product Gamma = sum b0 f0^T of the stage-entry
+// states (instead of one per gate).  Every gate's gradient follows exactly (linear algebra):
+//
+//   gate j of the stage, processed after j-1 others:
+//     f_j = A_j ... A_1 f0,   b_{j-1} = B_{j-1} ... B_1 b0
+//     G_j = sum b_{j-1} f_j^T = (B_{j-1} ... B_1) Gamma (A_j ... A_1)^T      (stage basis)
+//   then a partial trace over the stage qubits the gate does not touch, in the gate's own
+//   (pos2, pos1) index order — the quantity the reference accumulates per gate
+//   (get_q{1,2}_grad, circuit.rs:320-392; primitives.cu:202-354).
+//
+// Stage basis: index r = 2*bit(hi) + bit(lo) (a one-qubit stage: r = bit).  Products are
+// formed in double on the host; the device gets them rounded to the state precision.
+#pragma once
+
+#include <complex>
+#include <vector>
+
+namespace qdc {
+
+using cd = std::complex<double>;
+
+struct SMat {  // R x R, row-major, R = 2 or 4
+  int R = 4;
+  cd a[16];
+};
+
+inline SMat smat_identity(int R) {
+  SMat m;
+  m.R = R;
+  for (int i = 0; i < R * R; ++i) m.a[i] = 0;
+  for (int i = 0; i < R; ++i) m.a[i * R + i] = 1;
+  return m;
+}
+inline SMat smat_mul(const SMat& x, const SMat& y) {
+  SMat z;
+  z.R = x.R;
+  const int R = x.R;
+  for (int p = 0; p < R; ++p)
+    for (int q = 0; q < R; ++q) {
+      cd s = 0;
+      for (int k = 0; k < R; ++k) s += x.a[p * R + k] * y.a[k * R + q];
+      z.a[p * R + q] = s;
+    }
+  return z;
+}
+inline SMat smat_transpose(const SMat& x) {
+  SMat z;
+  z.R = x.R;
+  for (int p = 0; p < x.R; ++p)
+    for (int q = 0; q < x.R; ++q) z.a[p * x.R + q] = x.a[q * x.R + p];
+  return z;
+}
+
+// swap of the two qubit bits of a 4-index: (2h + l) -> (2l + h)
+inline int swap_bits4(int r) { return ((r & 1) << 1) | (r >> 1); }
+
+// How one gate sits in its stage.
+enum StageRole : int {
+  ROLE_Q1_ONLY = 0,  // one-qubit gate in a one-qubit stage
+  ROLE_Q1_LO = 1,    // one-qubit gate on the stage's lo qubit
+  ROLE_Q1_HI = 2,    // ... on the hi qubit
+  ROLE_Q2 = 3,       // two-qubit gate with pos2 = hi, pos1 = lo (stage basis == gate basis)
+  ROLE_Q2_SWAP = 4,  // two-qubit gate with pos2 = lo, pos1 = hi
+};
+
+// Embed a gate's matrix (its own basis; R_g = 2 or 4 entries row-major, or a diagonal of 4 when
+// `diag`) into the stage basis of dimension R.
+inline SMat stage_embed(const cd* g, bool diag, int role, int R) {
+  SMat m = smat_identity(R);
+  if (role == ROLE_Q1_ONLY) {
+    for (int i = 0; i < 4; ++i) m.a[i] = g[i];
+    return m;
+  }
+  for (int i = 0; i < 16; ++i) m.a[i] = 0;
+  if (role == ROLE_Q1_LO || role == ROLE_Q1_HI) {
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c) {
+        const int rh = r >> 1, rl = r & 1, ch = c >> 1, cl = c & 1;
+        if (role == ROLE_Q1_LO)
+          m.a[r * 4 + c] = (rh == ch) ? g[rl * 2 + cl] : cd(0);
+        else
+          m.a[r * 4 + c] = (rl == cl) ? g[rh * 2 + ch] : cd(0);
+      }
+    return m;
+  }
+  const bool sw = role == ROLE_Q2_SWAP;
+  for (int r = 0; r < 4; ++r) {
+    const int gr = sw ? swap_bits4(r) : r;
+    if (diag) {
+      m.a[r * 4 + r] = g[gr];
+    } else {
+      for (int c = 0; c < 4; ++c) m.a[r * 4 + c] = g[gr * 4 + (sw ? swap_bits4(c) : c)];
+    }
+  }
+  return m;
+}
+
+// Gradient of one gate (its own index order) from M = L Gamma Rt in the stage basis.
+// Writes 4 (q1, diagonal) or 16 (two-qubit) complex values.
+inline void stage_extract(const SMat& M, bool diag, int role, cd* out) {
+  if (role == ROLE_Q1_ONLY) {
+    for (int i = 0; i < 4; ++i) out[i] = M.a[i];
+    return;
+  }
+  if (role == ROLE_Q1_LO || role == ROLE_Q1_HI) {
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j) {
+        cd s = 0;
+        for (int k = 0; k < 2; ++k) {
+          const int r = role == ROLE_Q1_LO ? 2 * k + i : 2 * i + k;
+          const int c = role == ROLE_Q1_LO ? 2 * k + j : 2 * j + k;
+          s += M.a[r * 4 + c];
+        }
+        out[i * 2 + j] = s;
+      }
+    return;
+  }
+  const bool sw = role == ROLE_Q2_SWAP;
+  if (diag) {
+    for (int p = 0; p < 4; ++p) {
+      const int r = sw ? swap_bits4(p) : p;
+      out[p] = M.a[r * 4 + r];
+    }
+    return;
+  }
+  for (int p = 0; p < 4; ++p)
+    for (int q = 0; q < 4; ++q) {
+      const int r = sw ? swap_bits4(p) : p, c = sw ? swap_bits4(q) : q;
+      out[p * 4 + q] = M.a[r * 4 + c];
+    }
+}
+
+// One variable gate's gradient recipe inside a stage.
+struct StageGate {
+  uint32_t var;  // row of the gradient output (variable-gate order)
+  bool diag;
+  int role;
+  SMat L, Rt;  // G_stage = L Gamma Rt
+};
+
+// A stage whose Gamma is reduced into gradient slot `slot`.
+struct StagePost {
+  uint32_t slot;
+  int R;           // 2 or 4
+  bool diag_only;  // Gamma holds only its diagonal (4 values)
+  std::vector<StageGate> gates;
+};
+
+}  // namespace qdc
