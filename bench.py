@@ -32,6 +32,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "differentiable-quantum-circuit-cuda_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # vector peak (MI355X_MICROARCH.md; packed f32)
 
 
 def parse():
@@ -247,6 +248,8 @@ def main():
                         key=lambda kv: kv[1]["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
     bytes_per_launch = dom["algo_bytes"] / dom["launches"]
+    dom_flops = dom.get("algo_flops", 0.0) / dom["launches"]
+    valu_peak = VALU_PEAK_TFLOPS[args.precision]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = Path(args.pmc) if args.pmc else ROOT / "profiles" / "pmc_traffic.json"
@@ -258,6 +261,8 @@ def main():
     kernels = {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4),
                    "GB/s": round(v["algo_bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)
                    if v["total_ms"] > 0 else None,
+                   "TFLOP/s": round(v["algo_flops"] / (v["total_ms"] * 1e-3) / 1e12, 2)
+                   if v["total_ms"] > 0 and v.get("algo_flops") else None,
                    "share": round(v["total_ms"] / sum(s["total_ms"] for s in stats.values()), 4)}
                for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"])}
 
@@ -296,6 +301,13 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algo_bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(avg_ms, 4)},
+            # fused passes are VALU-bound: their FLOP rate against the vector peak
+            "compute": ({"bound": "valu", "kernel": dom_name,
+                         "achieved": round(dom_flops / (avg_ms * 1e-3) / 1e12, 2),
+                         "peak": valu_peak, "unit": "TFLOP/s",
+                         "frac": round(dom_flops / (avg_ms * 1e-3) / 1e12 / valu_peak, 4),
+                         "algo_flops_per_launch": dom_flops}
+                        if dom_flops > 0 else None),
             "kernels": kernels,
             "cpu_baseline": cpu,
         }

@@ -228,6 +228,7 @@ QDC_API size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out,
     s->launches += 1;
     s->total_ms += ms;
     s->algo_bytes += r.bytes;
+    s->algo_flops += r.flops;
   }
   for (size_t i = 0; i < agg.size() && i < cap; ++i) out[i] = agg[i];
   return agg.size();

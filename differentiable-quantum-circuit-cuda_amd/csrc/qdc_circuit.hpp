@@ -134,7 +134,7 @@ struct Exchange {
     }
     if (c.prof.on && a && b) {
       (void)hipEventRecord(b, c.stream);
-      c.prof.recs.push_back({"alltoall", bytes, a, b});  // link bytes, not HBM bytes
+      c.prof.recs.push_back({"alltoall", bytes, 0.0, a, b});  // link bytes, not HBM bytes
     }
     return nullptr;
   }
@@ -406,6 +406,7 @@ struct Circuit {
     uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {};
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t nstage = 0;  // fop count (stages) of the pass
+    double flops_per_amp = 0;  // algorithmic real FLOPs per amplitude of the pass
     uint32_t ngrad = 0;
     std::vector<uint32_t> grad_slots;  // gradient-buffer slot of each gradient stage
   };
@@ -571,6 +572,7 @@ struct Circuit {
       if (it.type != 2) continue;
       it.fop_off = fo * sizeof(fop);
       it.grad_slots.clear();
+      it.flops_per_amp = 0;
       const bool two = backward && it.ops[0] > first_inject;
       auto local_bit = [&](uint32_t p) -> uint32_t {
         if (p < (uint32_t)LV + it.lc) return p;
@@ -666,6 +668,10 @@ struct Circuit {
           mats[mo + n + i] = cx{(real)vb.real(), (real)vb.imag()};
         }
         mo += 2 * n;
+        // complex MACs per amplitude: 1 (diagonal), 2 (one qubit), 4 (two qubits) per matrix
+        // applied (A; B too when two-state) and per Gamma accumulated; 8 real FLOPs each
+        const double cmac = all_diag ? 1.0 : (R == 2 ? 2.0 : 4.0);
+        it.flops_per_amp += 8.0 * cmac * ((two ? 2.0 : 1.0) + (any_grad ? 1.0 : 0.0));
         if (any_grad) {
           post.slot = next_slot++;
           it.grad_slots.push_back(post.slot);
@@ -716,15 +722,18 @@ struct Circuit {
     const fop* fops = reinterpret_cast<const fop*>(prog_dev + it.fop_off);
     const cx* mats = reinterpret_cast<const cx*>(prog_dev + mats_off);
     const double bytes = (two ? 4.0 : 2.0) * state_bytes(nl);
+    const double flops = it.flops_per_amp * (double)((uint64_t)1 << nl);
     for (auto& s : sh) {
       chunk* f = reinterpret_cast<chunk*>(s.state);
       chunk* b = reinterpret_cast<chunk*>(s.bwd);
       if (!two) {
+        ctx.next_flops = flops;
         QDC_TRY(ctx.launch("fused_apply", bytes, k_fused<false, TILE_CHUNKS_1>, grid, f, b, fops,
                            mats, fg, (cx*)nullptr, (uint64_t)0));
         continue;
       }
       if (fg.ngrad == 0) {
+        ctx.next_flops = flops;
         QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
                            mats, fg, (cx*)nullptr, (uint64_t)0));
         continue;
@@ -734,6 +743,7 @@ struct Circuit {
       if (ctx.pending_dst.size() + fg.ngrad > (size_t)FIN_MAX) QDC_TRY(ctx.flush());
       ctx.pending_base = s.grads;
       ctx.pending_accumulate = 0;
+      ctx.next_flops = flops;
       QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
                          mats, fg, ctx.slot_ptr(), (uint64_t)NBMAX * RED));
       for (uint32_t slot : it.grad_slots) ctx.commit(slot, grid);

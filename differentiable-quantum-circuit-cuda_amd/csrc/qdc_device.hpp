@@ -59,6 +59,7 @@ inline const char* fail(const char* fmt, ...) {
 struct ProfRecord {
   const char* name;
   double bytes;
+  double flops;
   hipEvent_t a, b;
 };
 
@@ -96,6 +97,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   uint32_t grid_cap = 1u << 20;  // streaming launches: ~one item per thread (measured best)
   uint32_t red_cap = 2048;   // target blocks of reduction launches (<= NBMAX)
+  double next_flops = 0;     // algorithmic FLOPs of the next launch (profiling; reset by launch)
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -145,8 +147,9 @@ struct Ctx {
       return fail("HIP ERROR: launch of kernel %s failed with %s.", name, hipGetErrorName(e));
     if (prof.on && a && b) {
       (void)hipEventRecord(b, stream);
-      prof.recs.push_back({name, bytes, a, b});
+      prof.recs.push_back({name, bytes, next_flops, a, b});
     }
+    next_flops = 0;
     return nullptr;
   }
 

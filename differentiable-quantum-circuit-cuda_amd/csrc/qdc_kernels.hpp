@@ -755,6 +755,16 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
   if ((lane & (spread - 1)) == 0) acc[idx] += x[0];
 }
 
+// LDS layout of a fused tile: XOR-swizzled so that lanes of one LDS access spread over all
+// banks even when the op's target bits are the low ones.  Amplitude index i lives at
+// swz(i) = i ^ (((i >> (4 + LV)) & 15) << LV)  (chunk c at c ^ ((c >> 4) & 15): chunks stay
+// whole).  swz is linear over XOR, so swz(a0 | off) = swz(a0) ^ swz(off) with a uniform
+// swz(off): addressing costs one XOR, like the unswizzled add.
+__host__ __device__ __forceinline__ uint32_t swz(uint32_t i) {
+  return i ^ (((i >> (4 + LV)) & 15u) << LV);
+}
+__device__ __forceinline__ uint32_t swz_chunk(uint32_t c) { return c ^ ((c >> 4) & 15u); }
+
 template <bool TWO, int TB>
 #ifndef QDC_FUSED_WAVES
 #define QDC_FUSED_WAVES 4  // waves/SIMD the fused kernels are register-allocated for
@@ -813,7 +823,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
   auto fill = [&]() {  // pf -> LDS, each thread its own chunks
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const uint32_t c = t + (uint32_t)i * BLOCK;
+      const uint32_t c = swz_chunk(t + (uint32_t)i * BLOCK);
       lds[0][c] = pf[0][i];
       if constexpr (TWO) lds[NS - 1][c] = pf[NS - 1][i];
     }
@@ -847,13 +857,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
         }
         cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        const uint32_t s1 = 1u << op.t1;
+        const uint32_t s1 = swz(1u << op.t1);
         for (uint32_t it = 0; it < ta / (2 * BLOCK); ++it) {
           const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = (uint32_t)insert_zero(grp, op.t1);
-          cx fx[2] = {lf[a0], lf[a0 + s1]};
+          const uint32_t a0 = swz((uint32_t)insert_zero(grp, op.t1));
+          cx fx[2] = {lf[a0], lf[a0 ^ s1]};
           if constexpr (TWO) {
-            cx bx[2] = {lb[a0], lb[a0 + s1]};
+            cx bx[2] = {lb[a0], lb[a0 ^ s1]};
             if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 2; ++p)
@@ -863,12 +873,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
             umatvec<2>(A, fx);
             umatvec<2>(B, bx);
             lb[a0] = bx[0];
-            lb[a0 + s1] = bx[1];
+            lb[a0 ^ s1] = bx[1];
           } else {
             umatvec<2>(A, fx);
           }
           lf[a0] = fx[0];
-          lf[a0 + s1] = fx[1];
+          lf[a0 ^ s1] = fx[1];
         }
         if (grad) {
           real v[8];
@@ -892,17 +902,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
         for (int i = 0; i < 16; ++i) acc[i] = {0, 0};
         const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
-        const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
+        const uint32_t s1 = swz(1u << op.t1), s2 = swz(1u << op.t2);
+        const uint32_t soff[4] = {0, s1, s2, s1 ^ s2};
         for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
           const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
-          const uint32_t off[4] = {0, s1, s2, s1 + s2};
+          const uint32_t a0 = swz((uint32_t)insert_zero(insert_zero(grp, lo), hi));
           cx fx[4], bx[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) fx[r] = lf[a0 + off[r]];
+          for (int r = 0; r < 4; ++r) fx[r] = lf[a0 ^ soff[r]];
           if constexpr (TWO) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) bx[r] = lb[a0 + off[r]];
+            for (int r = 0; r < 4; ++r) bx[r] = lb[a0 ^ soff[r]];
             if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 4; ++p)
@@ -912,12 +922,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
             umatvec<4>(A, fx);
             umatvec<4>(B, bx);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) lb[a0 + off[r]] = bx[r];
+            for (int r = 0; r < 4; ++r) lb[a0 ^ soff[r]] = bx[r];
           } else {
             umatvec<4>(A, fx);
           }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) lf[a0 + off[r]] = fx[r];
+          for (int r = 0; r < 4; ++r) lf[a0 ^ soff[r]] = fx[r];
         }
         if (grad) {
           real v[32];
@@ -940,19 +950,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
         cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
-        const uint32_t s1 = 1u << op.t1, s2 = 1u << op.t2;
+        const uint32_t s1 = swz(1u << op.t1), s2 = swz(1u << op.t2);
+        const uint32_t soff[4] = {0, s1, s2, s1 ^ s2};
         for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
           const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = (uint32_t)insert_zero(insert_zero(grp, lo), hi);
-          const uint32_t off[4] = {0, s1, s2, s1 + s2};
+          const uint32_t a0 = swz((uint32_t)insert_zero(insert_zero(grp, lo), hi));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const cx f0 = lf[a0 + off[r]];
-            lf[a0 + off[r]] = ucmul(A[r], f0);
+            const cx f0 = lf[a0 ^ soff[r]];
+            lf[a0 ^ soff[r]] = ucmul(A[r], f0);
             if constexpr (TWO) {
-              const cx bv = lb[a0 + off[r]];
+              const cx bv = lb[a0 ^ soff[r]];
               if (grad) acc[r] = vcfma(bv, f0, acc[r]);
-              lb[a0 + off[r]] = ucmul(B[r], bv);
+              lb[a0 ^ soff[r]] = ucmul(B[r], bv);
             }
           }
         }
@@ -972,7 +982,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
     // each thread stores (and next refills) only its own chunks: no barrier needed here
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const uint32_t c = t + (uint32_t)i * BLOCK;
+      const uint32_t c = swz_chunk(t + (uint32_t)i * BLOCK);
       stc(f + cur + off[i], lds[0][c]);
       if constexpr (TWO) stc(b + cur + off[i], lds[NS - 1][c]);
     }

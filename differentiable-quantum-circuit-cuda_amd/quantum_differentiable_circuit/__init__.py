@@ -227,7 +227,8 @@ class _CircuitBase:
         k = int(self._lib.qdc_circuit_profile_collect(self._h, buf, cap))
         return {buf[i].name.decode(): {"launches": int(buf[i].launches),
                                         "total_ms": float(buf[i].total_ms),
-                                        "algo_bytes": float(buf[i].algo_bytes)}
+                                        "algo_bytes": float(buf[i].algo_bytes),
+                                        "algo_flops": float(buf[i].algo_flops)}
                 for i in range(min(k, cap))}
 
 

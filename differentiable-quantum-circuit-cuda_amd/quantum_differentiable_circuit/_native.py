@@ -49,7 +49,7 @@ class PlanOp(C.Structure):
 
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_size_t), ("total_ms", C.c_double),
-                ("algo_bytes", C.c_double)]
+                ("algo_bytes", C.c_double), ("algo_flops", C.c_double)]
 
 
 _P = C.c_void_p

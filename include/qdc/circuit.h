@@ -101,6 +101,7 @@ typedef struct qdc_kernel_stat {
   size_t launches;
   double total_ms;    /* sum of HIP-event durations of this kernel's launches */
   double algo_bytes;  /* sum of algorithmic HBM bytes (SURVEY.md §8 d) */
+  double algo_flops;  /* sum of algorithmic real FLOPs (fused passes; 0 for streaming kernels) */
 } qdc_kernel_stat;
 
 /* Bracket every launch of this circuit's stream with HIP events (on = 1) or stop (0);

@@ -30,6 +30,10 @@ def bench_name(kernel):
     m = re.search(r"k_diag<(\d+)", kernel)
     if m:
         return DIAG[int(m.group(1))]
+    if "k_fused<false" in kernel:
+        return "fused_apply"
+    if "k_fused<true" in kernel:
+        return "fused_reverse"
     if "k_elementwise<0>" in kernel:
         return "copy"
     if "k_finalize" in kernel:
