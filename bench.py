@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--seed", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gate-sample", action="store_true",
+                    help="skip the single-gate (fusion off) kernel sample")
     ap.add_argument("--cpu-gates", type=int, default=12,
                     help="gates of the CPU baseline sample (the workload's first gates, full n)")
     ap.add_argument("--cpu-densities", type=int, default=4)
@@ -142,8 +144,51 @@ def cpu_baseline(args, n):
                       f"(oracle/cpu_ref.c, OpenMP, reference algorithm unfused)"}
 
 
+def gate_kernel_sample(args, n):
+    """Single-gate kernels (fusion off): the north star's >= 70 % HBM target is on 1- and
+    2-qubit gate application at n=28 f32.  One circuit with q1 / q2 gates at low, middle and
+    high positions (every kernel family), fwd+bwd x3, per-kernel algorithmic GB/s."""
+    import quantum_differentiable_circuit as q
+    dt = np.complex64 if args.precision == "f32" else np.complex128
+    rng = np.random.default_rng(1)
+    os.environ["QDC_FUSE"] = "0"
+    try:
+        c = q.circuit_class(args.precision)(n)
+    finally:
+        os.environ.pop("QDC_FUSE", None)
+    var = []
+    for _ in range(2):
+        for pos in (0, 1, n // 2, n - 1):
+            c.add_q1_var_gate(pos)
+            var.append(np.ascontiguousarray(O_haar(rng, 2), dtype=dt))
+        for pos2, pos1 in ((1, 0), (n - 1, 0), (n // 2 + 1, n // 2), (n - 1, n - 2)):
+            c.add_q2_var_gate(pos2, pos1)
+            var.append(np.ascontiguousarray(O_haar(rng, 4), dtype=dt))
+    c.get_q1_dens_op_with_grad(0)
+    cot = sigma_z_cotangents(1, dt)
+    c.forward([], var)
+    c.backward(cot, [], var)
+    c.profile(True)
+    for _ in range(3):
+        c.forward([], var)
+        c.backward(cot, [], var)
+    stats = c.profile_collect()
+    c.profile(False)
+    del c
+    out = {}
+    for k in ("apply_q1", "apply_q2", "reverse_q1", "reverse_q2"):
+        if k in stats and stats[k]["total_ms"] > 0:
+            gbs = stats[k]["algo_bytes"] / (stats[k]["total_ms"] * 1e-3) / 1e9
+            out[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "launches": stats[k]["launches"],
+                      "avg_ms": round(stats[k]["total_ms"] / stats[k]["launches"], 4)}
+    return out
+
+
 def micro(args):
-    """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse."""
+    """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse
+    (single-gate kernels: fusion off)."""
+    os.environ["QDC_FUSE"] = "0"
     import quantum_differentiable_circuit as q
     n, prec = args.qubits, args.precision
     dt = np.complex64 if prec == "f32" else np.complex128
@@ -270,6 +315,16 @@ def main():
     assert all(np.isfinite(g).all() for g in grads)
     assert all(abs(np.trace(d) - 1) < 1e-3 for d in dens)
 
+    # the fused path against the per-gate roofline: every gate costs 2S forward and 4S in the
+    # reverse sweep (SURVEY.md §8 d) if applied one HBM pass at a time
+    state_bytes = (1 << n) * (8 if args.precision == "f32" else 16)
+    eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / max(world, 1)
+    effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
+                 "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
+    gate_kernels = None
+    if rank == 0 and world == 1 and not args.no_gate_sample:
+        gate_kernels = gate_kernel_sample(args, n)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_qubits or n)
@@ -309,6 +364,8 @@ def main():
                          "algo_flops_per_launch": dom_flops}
                         if dom_flops > 0 else None),
             "kernels": kernels,
+            "effective_gate_bandwidth": effective,
+            "gate_kernels": gate_kernels,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

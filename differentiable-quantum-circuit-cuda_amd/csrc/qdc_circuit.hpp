@@ -179,6 +179,8 @@ struct Circuit {
   int fuse = 1;             // 0: one HBM pass per gate
   uint32_t fuse_max_ops = FMAX_OPS;
   uint32_t fuse_lcmin = 3;  // min contiguous chunk bits of a fused tile (128-B rows)
+  int fuse_meas = 1;        // densities / cotangent injections join fused passes
+  std::vector<uint8_t> fwd_sens;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   uint32_t fused_resident[2] = {0, 0};
   unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
@@ -204,6 +206,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
       fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
+    if (const char* e = getenv("QDC_FUSE_MEAS")) fuse_meas = atoi(e);
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
@@ -407,8 +410,10 @@ struct Circuit {
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t nstage = 0;  // fop count (stages) of the pass
     double flops_per_amp = 0;  // algorithmic real FLOPs per amplitude of the pass
+    bool has_red = false;      // reduction ops (Gamma stages or densities)
+    bool writes_f = false;     // gate stages (fwd changes; else fwd is only read)
     uint32_t ngrad = 0;
-    std::vector<uint32_t> grad_slots;  // gradient-buffer slot of each gradient stage
+    std::vector<uint32_t> grad_slots;  // reduction slot of each reduction op, in op order
   };
   static constexpr uint32_t TILE_CHUNKS_1 = 2048;  // one-state fused tile (chunks)
   static constexpr uint32_t TILE_CHUNKS_2 = 1024;  // two-state fused tile (chunks per state)
@@ -445,18 +450,74 @@ struct Circuit {
     return false;
   }
 
-  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward) const {
+  // Ordering rules beyond "same qubit => program order" (qdc_stage.hpp has the algebra):
+  //  * a density commutes with unitary gates on other qubits, not with non-unitary ones;
+  //  * a cotangent injection (reverse sweep) commutes only with const unitary gates on other
+  //    qubits: a variable gate's gradient sees the bwd state, so it keeps its order.
+  // "meas" ops (densities, injections) and "sensitive" gates (non-unitary; in the reverse
+  // sweep also variable) therefore never pass each other: once one kind is left for a later
+  // pass or stage, every later op of the other kind is too.
+  bool is_meas(const qdc_plan_op& op) const {
+    return op.type == QDC_PLAN_OP && is_density(ins[op.instr].kind);
+  }
+  // Forward: a density passes a gate on other qubits only if the gate is unitary to
+  // working precision (the reduced density is invariant under U_B only if U_B^+ U_B = I), so
+  // it is checked per call on the actual matrices (fwd_sens).  Reverse sweep: the reference
+  // uncomputes every non-NonU kind with U^+ (diagonal: conj), so B = U^T = conj(A) holds by
+  // construction and an injection commutes with such const gates whatever the matrix.
+  bool is_sens(const qdc_plan_op& op, bool backward) const {
+    if (op.type != QDC_PLAN_OP) return false;
+    const int k = ins[op.instr].kind;
+    if (!(is_const(k) || is_var(k))) return false;
+    if (backward) return is_nonu(k) || is_var(k);
+    return is_nonu(k) || (op.instr < fwd_sens.size() && fwd_sens[op.instr]);
+  }
+  // max |U^+ U - I| of a gate's host matrix (diagonal: max ||d_i|^2 - 1|)
+  static double unitarity_error(const qdc_complex* g, int kind) {
+    if (is_diag(kind)) {
+      double e = 0;
+      for (int i = 0; i < 4; ++i) {
+        const double m = (double)g[i].re * g[i].re + (double)g[i].im * g[i].im;
+        e = std::max(e, std::abs(m - 1.0));
+      }
+      return e;
+    }
+    const int R = is_q1_gate(kind) ? 2 : 4;
+    double e = 0;
+    for (int p = 0; p < R; ++p)
+      for (int q = 0; q < R; ++q) {
+        double re = 0, im = 0;  // (U^+ U)[p][q] = sum_k conj(U[k][p]) U[k][q]
+        for (int k = 0; k < R; ++k) {
+          const qdc_complex a = g[k * R + p], b = g[k * R + q];
+          re += (double)a.re * b.re + (double)a.im * b.im;
+          im += (double)a.re * b.im - (double)a.im * b.re;
+        }
+        e = std::max(e, std::hypot(re - (p == q ? 1.0 : 0.0), im));
+      }
+    return e;
+  }
+  bool is_gate_op(const qdc_plan_op& op) const {
+    if (op.type != QDC_PLAN_OP) return false;
+    const int k = ins[op.instr].kind;
+    return is_const(k) || is_var(k);
+  }
+  uint64_t op_bits(const qdc_plan_op& op) const {
+    return chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
+  }
+
+  // backward: plan indices >= first_inject run two-state (bwd exists); a pass never spans it.
+  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
+                               size_t first_inject = SIZE_MAX) const {
     std::vector<Item> items;
     const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
-    auto is_gate = [&](const qdc_plan_op& op) {
-      if (op.type != QDC_PLAN_OP) return false;
-      const Instr& in = ins[op.instr];
-      return is_const(in.kind) || is_var(in.kind);
-    };
-    auto bits_of = [&](const qdc_plan_op& op) {
-      return chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
-    };
     const bool on = fuse && fuse_max_ops >= 2;
+    auto fusable = [&](size_t k) {
+      const qdc_plan_op& op = plan[k];
+      if (!(is_gate_op(op) || (fuse_meas && is_meas(op))) || !tile_fits(op_bits(op), T))
+        return false;
+      // injections need bwd: only in the two-state part
+      return !(backward && is_meas(op) && k < first_inject);
+    };
     size_t i = 0;
     while (i < plan.size()) {
       const qdc_plan_op& op = plan[i];
@@ -465,39 +526,56 @@ struct Circuit {
         ++i;
         continue;
       }
-      if (!on || !is_gate(op) || !tile_fits(bits_of(op), T)) {
+      if (!on || !fusable(i)) {
         items.push_back(Item{0, {(uint32_t)i}});
         ++i;
         continue;
       }
       size_t j = i;
-      while (j < plan.size() && is_gate(plan[j]) && tile_fits(bits_of(plan[j]), T)) ++j;
+      while (j < plan.size() && plan[j].type == QDC_PLAN_OP && fusable(j) &&
+             !(backward && j == first_inject && j > i))
+        ++j;
+      const bool two = backward && i >= first_inject;
       std::vector<uint32_t> rem;
       for (size_t k = i; k < j; ++k) rem.push_back((uint32_t)k);
       while (!rem.empty()) {
         uint64_t mask = 0, blocked = 0;
-        uint32_t ngrad = 0;
+        uint32_t nred = 0;
+        bool meas_left = false, sens_left = false;
         std::vector<uint32_t> pass, rest;
+        int kind = -1;  // reverse sweep: a pass is injections only or gates only
         for (uint32_t k : rem) {
           const qdc_plan_op& g = plan[k];
           const uint64_t q = (1ull << g.pos2) | (1ull << g.pos1);
-          const uint32_t isgrad = (backward && is_var(ins[g.instr].kind)) ? 1u : 0u;
-          if ((q & blocked) || pass.size() >= fuse_max_ops || ngrad + isgrad > (uint32_t)FMAX_GRAD ||
-              !tile_fits(mask | bits_of(g), T)) {
+          const bool meas = is_meas(g), sens = is_sens(g, backward);
+          if (backward && kind >= 0 && (int)meas != kind) {
             blocked |= q;
+            meas_left = meas_left || meas;
+            sens_left = sens_left || sens;
+            rest.push_back(k);
+            continue;
+          }
+          const uint32_t isred =
+              ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
+          if ((q & blocked) || (meas && sens_left) || (sens && meas_left) ||
+              pass.size() >= fuse_max_ops || nred + isred > (uint32_t)FMAX_GRAD ||
+              !tile_fits(mask | op_bits(g), T)) {
+            blocked |= q;
+            meas_left = meas_left || meas;
+            sens_left = sens_left || sens;
             rest.push_back(k);
             continue;
           }
           pass.push_back(k);
-          mask |= bits_of(g);
-          ngrad += isgrad;
+          mask |= op_bits(g);
+          nred += isred;
+          kind = (int)meas;
         }
         if (pass.size() == 1) {
           items.push_back(Item{0, pass});
         } else {
           Item it{2, pass};
           tile_config(mask, T, it.lc, it.h, it.hb);
-          it.ngrad = ngrad;
           items.push_back(it);
         }
         rem.swap(rest);
@@ -511,17 +589,36 @@ struct Circuit {
   // joins the current stage if none of its qubits is blocked (an earlier gate on it is left
   // for a later stage) and the stage stays within two qubits.  Per qubit, order is kept.
   std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
-                                                     const std::vector<qdc_plan_op>& plan) const {
+                                                     const std::vector<qdc_plan_op>& plan,
+                                                     bool backward) const {
     std::vector<std::vector<uint32_t>> stages;
     std::vector<uint32_t> rem = pass;
     while (!rem.empty()) {
       std::vector<uint32_t> st, rest;
       uint64_t q = 0, blocked = 0;
+      bool meas_left = false, sens_left = false, closed = false;
       for (uint32_t k : rem) {
+        if (closed) {
+          rest.push_back(k);
+          continue;
+        }
         const qdc_plan_op& g = plan[k];
         const uint64_t gq = (1ull << g.pos2) | (1ull << g.pos1);
-        if ((gq & blocked) || __builtin_popcountll(q | gq) > 2) {
+        const bool meas = is_meas(g), sens = is_sens(g, backward);
+        bool bad = (gq & blocked) || (meas && sens_left) || (sens && meas_left);
+        if (!bad && meas) {
+          if (st.empty()) {  // a density / injection is a stage of its own
+            st.push_back(k);
+            closed = true;
+            continue;
+          }
+          bad = true;
+        }
+        if (!bad && __builtin_popcountll(q | gq) > 2) bad = true;
+        if (bad) {
           blocked |= gq;
+          meas_left = meas_left || meas;
+          sens_left = sens_left || sens;
           rest.push_back(k);
           continue;
         }
@@ -539,21 +636,24 @@ struct Circuit {
   // backward: `first_inject` = plan index of the first cotangent injection (passes before it
   // only uncompute fwd); gradient stages get slots nvar, nvar+1, ... of the gradient buffer and
   // a recipe in stage_post (qdc_stage.hpp).
+  // forward: densities reduce into dens slot out_idx[instr]; backward: injections read their
+  // cotangent from dg.
   const char* build_program(std::vector<Item>& items, const std::vector<qdc_plan_op>& plan,
                             bool backward, size_t first_inject, const Flat& cg, const Flat& vg,
                             const std::vector<size_t>& gidx, size_t& mats_off,
-                            const std::vector<uint32_t>& var_idx, uint32_t nvar) {
+                            const std::vector<uint32_t>& var_idx, uint32_t nvar,
+                            const std::vector<uint32_t>& out_idx, const Flat* dg) {
     stage_post.clear();
     std::vector<std::vector<std::vector<uint32_t>>> stages_of(items.size());
     size_t nops = 0;
     for (size_t ii = 0; ii < items.size(); ++ii)
       if (items[ii].type == 2) {
-        stages_of[ii] = stage_partition(items[ii].ops, plan);
+        stages_of[ii] = stage_partition(items[ii].ops, plan, backward);
         nops += stages_of[ii].size();
       }
     if (nops == 0) return nullptr;
     mats_off = ((nops * sizeof(fop) + 255) / 256) * 256;
-    const size_t bytes = mats_off + nops * 32 * sizeof(cx);
+    const size_t bytes = mats_off + nops * 32 * sizeof(cx);  // <= 2 R^2 = 32 per op
     if (bytes > prog_cap) {
       QDC_HIP(hipStreamSynchronize(ctx.stream));
       if (prog_dev) QDC_HIP(hipFree(prog_dev));
@@ -573,7 +673,9 @@ struct Circuit {
       it.fop_off = fo * sizeof(fop);
       it.grad_slots.clear();
       it.flops_per_amp = 0;
-      const bool two = backward && it.ops[0] > first_inject;
+      const bool two = backward && it.ops[0] >= first_inject;
+      it.has_red = false;
+      it.writes_f = false;
       auto local_bit = [&](uint32_t p) -> uint32_t {
         if (p < (uint32_t)LV + it.lc) return p;
         for (uint32_t r = 0; r < it.h; ++r)
@@ -581,6 +683,36 @@ struct Circuit {
         return 0xffffffffu;  // unreachable: tile_config covered every bit
       };
       for (const auto& st : stages_of[ii]) {
+        if (is_meas(plan[st[0]])) {  // density (forward) or cotangent injection (backward)
+          const qdc_plan_op& op = plan[st[0]];
+          const Instr& in = ins[op.instr];
+          const bool q1 = is_q1_density(in.kind);
+          const int R = q1 ? 2 : 4;
+          fop& F = fops[fo++];
+          F.t1 = local_bit(q1 ? op.pos2 : op.pos1);
+          F.t2 = local_bit(op.pos2);
+          F.mat = (uint32_t)mo;
+          for (int i = 0; i < 2 * R * R; ++i) mats[mo + i] = cx{0, 0};
+          if (backward) {  // b += (G^T on pos) (2 conj f), G = conj of the JAX cotangent
+            F.kind = q1 ? FK_INJ1 : FK_INJ2;
+            const qdc_complex* gd = dg->at(gidx[op.instr]);
+            if (q1) {
+              const mat<2> m = transpose<2>(to_mat<2>(gd));
+              for (int i = 0; i < 4; ++i) mats[mo + i] = m.a[i];
+            } else {
+              const mat<4> m = transpose<4>(to_mat<4>(gd));
+              for (int i = 0; i < 16; ++i) mats[mo + i] = m.a[i];
+            }
+            it.flops_per_amp += 8.0 * (q1 ? 2.0 : 4.0);
+          } else {
+            F.kind = q1 ? FK_DENS1 : FK_DENS2;
+            it.grad_slots.push_back(out_idx[op.instr]);
+            it.has_red = true;
+            it.flops_per_amp += 8.0 * (q1 ? 2.0 : 4.0);
+          }
+          mo += 2 * R * R;
+          continue;
+        }
         // stage qubits (physical positions), lo < hi
         uint64_t qm = 0;
         bool all_diag = true, any_grad = false;
@@ -658,8 +790,9 @@ struct Circuit {
         F.t1 = local_bit(lo);
         F.t2 = local_bit(hi);
         F.mat = (uint32_t)mo;
-        const uint32_t kind = all_diag ? 2u : (R == 2 ? 0u : 1u);
-        F.kind = kind | (any_grad ? 4u : 0u);
+        const uint32_t kind = all_diag ? FK_DIAG : (R == 2 ? FK_Q1 : FK_Q2);
+        F.kind = kind | (any_grad ? FOP_GAMMA : 0u);
+        it.writes_f = true;
         const int n = all_diag ? 4 : R * R;
         for (int i = 0; i < n; ++i) {
           const cd va = all_diag ? A.a[i * 4 + i] : A.a[i];
@@ -675,6 +808,7 @@ struct Circuit {
         if (any_grad) {
           post.slot = next_slot++;
           it.grad_slots.push_back(post.slot);
+          it.has_red = true;
           stage_post.push_back(std::move(post));
         }
       }
@@ -688,14 +822,24 @@ struct Circuit {
 
   // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
   // gradient gates write partials for gradient buffer rows var_idx[...].
-  const char* run_fused(const Item& it, const std::vector<qdc_plan_op>& plan, bool two,
-                        size_t mats_off) {
+  template <bool TWO, bool HASRED, bool WF>
+  const char* launch_fused(const char* name, double bytes, uint32_t grid, chunk* f, chunk* b,
+                           const fop* fops, const cx* mats, const fgeo& fg, cx* partials,
+                           uint64_t stride) {
+    constexpr int TB = TWO ? (int)TILE_CHUNKS_2 : (int)TILE_CHUNKS_1;
+    return ctx.launch(name, bytes, k_fused<TWO, TB, HASRED, WF>, grid, f, b, fops, mats, fg,
+                      partials, stride);
+  }
+
+  // Run one fused pass on every shard.  two: fwd and bwd (reverse sweep).  Reductions (Gamma
+  // stages, densities) go to slots it.grad_slots of red_base (grads or dens of each shard).
+  const char* run_fused(const Item& it, bool two, size_t mats_off, bool red_to_grads) {
     fgeo fg{};
     fg.lc = it.lc;
     fg.h = it.h;
     for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];
     fg.nops = it.nstage;
-    fg.ngrad = two ? it.ngrad : 0;
+    fg.ngrad = it.has_red ? (uint32_t)it.grad_slots.size() : 0;
     fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
     // one wave of resident blocks, each pipelining a contiguous run of tiles
     uint32_t target = fused_blocks;
@@ -705,10 +849,10 @@ struct Circuit {
         int per_cu = 0, dev = 0, cus = 0;
         if (two)
           QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, k_fused<true, TILE_CHUNKS_2>, BLOCK, 0));
+              &per_cu, k_fused<true, TILE_CHUNKS_2, true, true>, BLOCK, 0));
         else
           QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, k_fused<false, TILE_CHUNKS_1>, BLOCK, 0));
+              &per_cu, k_fused<false, TILE_CHUNKS_1, true, true>, BLOCK, 0));
         QDC_HIP(hipGetDevice(&dev));
         QDC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         res = (uint32_t)std::max(1, std::min(per_cu * cus, (int)NBMAX));
@@ -721,32 +865,45 @@ struct Circuit {
     const uint32_t grid = (uint32_t)((fg.ntiles + tpb - 1) / tpb);
     const fop* fops = reinterpret_cast<const fop*>(prog_dev + it.fop_off);
     const cx* mats = reinterpret_cast<const cx*>(prog_dev + mats_off);
-    const double bytes = (two ? 4.0 : 2.0) * state_bytes(nl);
+    // algorithmic bytes: each state read once, written once if the pass changes it
+    const double S = state_bytes(nl);
+    const double bytes = two ? (it.writes_f ? 4.0 : 3.0) * S : (it.writes_f ? 2.0 : 1.0) * S;
     const double flops = it.flops_per_amp * (double)((uint64_t)1 << nl);
+    const char* name = two ? "fused_reverse" : "fused_apply";
+    if (fg.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     for (auto& s : sh) {
       chunk* f = reinterpret_cast<chunk*>(s.state);
       chunk* b = reinterpret_cast<chunk*>(s.bwd);
-      if (!two) {
-        ctx.next_flops = flops;
-        QDC_TRY(ctx.launch("fused_apply", bytes, k_fused<false, TILE_CHUNKS_1>, grid, f, b, fops,
-                           mats, fg, (cx*)nullptr, (uint64_t)0));
-        continue;
+      cx* parts = nullptr;
+      if (fg.ngrad > 0) {
+        cx* base = red_to_grads ? s.grads : s.dens;
+        QDC_TRY(ctx.begin_reduction(base, 0));
+        if (ctx.pending_dst.size() + fg.ngrad > (size_t)FIN_MAX) QDC_TRY(ctx.flush());
+        ctx.pending_base = base;
+        ctx.pending_accumulate = 0;
+        parts = ctx.slot_ptr();
       }
-      if (fg.ngrad == 0) {
-        ctx.next_flops = flops;
-        QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
-                           mats, fg, (cx*)nullptr, (uint64_t)0));
-        continue;
-      }
-      if (grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
-      QDC_TRY(ctx.begin_reduction(s.grads, 0));
-      if (ctx.pending_dst.size() + fg.ngrad > (size_t)FIN_MAX) QDC_TRY(ctx.flush());
-      ctx.pending_base = s.grads;
-      ctx.pending_accumulate = 0;
+      const uint64_t stride = (uint64_t)NBMAX * RED;
       ctx.next_flops = flops;
-      QDC_TRY(ctx.launch("fused_reverse", bytes, k_fused<true, TILE_CHUNKS_2>, grid, f, b, fops,
-                         mats, fg, ctx.slot_ptr(), (uint64_t)NBMAX * RED));
-      for (uint32_t slot : it.grad_slots) ctx.commit(slot, grid);
+      if (two) {
+        if (it.writes_f)
+          QDC_TRY((launch_fused<true, true, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
+                                                   stride)));
+        else
+          QDC_TRY((launch_fused<true, false, false>(name, bytes, grid, f, b, fops, mats, fg,
+                                                     parts, stride)));
+      } else if (!it.has_red) {
+        QDC_TRY((launch_fused<false, false, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
+                                                   stride)));
+      } else if (it.writes_f) {
+        QDC_TRY((launch_fused<false, true, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
+                                                  stride)));
+      } else {
+        QDC_TRY((launch_fused<false, true, false>(name, bytes, grid, f, b, fops, mats, fg, parts,
+                                                   stride)));
+      }
+      if (fg.ngrad > 0)
+        for (uint32_t slot : it.grad_slots) ctx.commit(slot, grid);
     }
     return nullptr;
   }
@@ -797,12 +954,19 @@ struct Circuit {
           out_idx[k] = o++;
     }
     const std::vector<qdc_plan_op> pl = plan(mode);
+    fwd_sens.assign(ins.size(), 0);
+    const double utol = sizeof(real) == 4 ? 1e-6 : 1e-13;
+    for (size_t k = 0; k < ins.size(); ++k)
+      if (is_const(ins[k].kind) || is_var(ins[k].kind)) {
+        const qdc_complex* g4 = is_const(ins[k].kind) ? cg.at(gidx[k]) : vg.at(gidx[k]);
+        fwd_sens[k] = unitarity_error(g4, ins[k].kind) > utol ? 1 : 0;
+      }
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
-    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0));
+    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
     for (const Item& item : items) {
       if (item.type == 2) {
-        QDC_TRY(run_fused(item, pl, false, mats_off));
+        QDC_TRY(run_fused(item, false, mats_off, false));
         continue;
       }
       const qdc_plan_op& op = pl[item.ops[0]];
@@ -885,13 +1049,19 @@ struct Circuit {
         first_inject = i;
         break;
       }
-    std::vector<Item> items = fuse_items(pl, true);
+    std::vector<Item> items = fuse_items(pl, true, first_inject);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
-                          (uint32_t)nvar));
+                          (uint32_t)nvar, {}, &dg));
     for (const Item& item : items) {
       if (item.type == 2) {
-        QDC_TRY(run_fused(item, pl, have_bwd, mats_off));
+        const bool two = item.ops[0] >= first_inject;
+        if (two && !have_bwd) {  // the first injection is fused: it adds into a zero bwd
+          for (auto& s : sh)
+            QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), ctx.stream));
+          have_bwd = true;
+        }
+        QDC_TRY(run_fused(item, two, mats_off, true));
         continue;
       }
       const qdc_plan_op& op = pl[item.ops[0]];

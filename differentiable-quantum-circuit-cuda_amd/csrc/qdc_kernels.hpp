@@ -568,7 +568,7 @@ struct fgeo {
   uint32_t h;      // row bits
   uint32_t hb[FMAX_ROWS];
   uint32_t nops;
-  uint32_t ngrad;  // gradient gates (their partials go to consecutive slots)
+  uint32_t ngrad;  // reduction ops (Gamma stages, densities): partials in consecutive slots
 };
 
 // Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the
@@ -765,23 +765,37 @@ __host__ __device__ __forceinline__ uint32_t swz(uint32_t i) {
 }
 __device__ __forceinline__ uint32_t swz_chunk(uint32_t c) { return c ^ ((c >> 4) & 15u); }
 
-template <bool TWO, int TB>
+// fop.kind: op kind (low 3 bits) + FOP_GAMMA
+enum : uint32_t {
+  FK_Q1 = 0,     // one-qubit stage: f <- A f [, b <- B b]
+  FK_Q2 = 1,     // two-qubit stage
+  FK_DIAG = 2,   // diagonal two-qubit stage
+  FK_DENS1 = 3,  // one-qubit density: acc[2p+q] += f_p conj(f_q)        (read-only)
+  FK_DENS2 = 4,  // two-qubit density: acc[4p+q] += f_p conj(f_q)        (read-only)
+  FK_INJ1 = 5,   // one-qubit cotangent injection: b += M (2 conj f)     (two-state)
+  FK_INJ2 = 6,   // two-qubit cotangent injection
+};
+constexpr uint32_t FOP_GAMMA = 8;  // stage also accumulates Gamma = sum b0 f0^T (two-state)
+
 #ifndef QDC_FUSED_WAVES
 #define QDC_FUSED_WAVES 4  // waves/SIMD the fused kernels are register-allocated for
 #endif
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED_WAVES))) void k_fused(chunk* __restrict__ f, chunk* __restrict__ b,
-                                                 const fop* __restrict__ ops,
-                                                 const cx* __restrict__ mats, fgeo fg,
-                                                 cx* __restrict__ partials,
-                                                 uint64_t slot_stride) {
+// TWO: the pass carries fwd and bwd (reverse sweep); HASRED: the pass has reduction ops (Gamma,
+// densities) and their LDS accumulators; WF: the pass changes fwd, so fwd is stored back
+// (density-only and injection-only passes read it only).
+template <bool TWO, int TB, bool HASRED, bool WF>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED_WAVES)))
+void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
+             const cx* __restrict__ mats, fgeo fg, cx* __restrict__ partials,
+             uint64_t slot_stride) {
   constexpr int NS = TWO ? 2 : 1;
   constexpr int CPT = TB / BLOCK;  // chunks of each state per thread and tile
   static_assert(TB % BLOCK == 0 && TB * VEC >= 4 * BLOCK, "tile must cover the block");
   __shared__ chunk lds[NS][TB];
-  __shared__ real accw[TWO ? BLOCK / 64 : 1][FMAX_GRAD][FACC];
+  __shared__ real accw[HASRED ? BLOCK / 64 : 1][HASRED ? FMAX_GRAD : 1][FACC];
   const uint32_t t = threadIdx.x;
   const int wave = t >> 6;
-  if constexpr (TWO) {
+  if constexpr (HASRED) {
     for (uint32_t i = t; i < (BLOCK / 64) * FMAX_GRAD * FACC; i += BLOCK)
       (&accw[0][0][0])[i] = 0;
   }
@@ -808,7 +822,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
     return base;
   };
-  // software pipeline: the next tile's chunks are in flight while this tile's gates run
+  // software pipeline: the next tile's chunks are in flight while this tile's ops run
   chunk pf[NS][CPT];
   auto prefetch = [&](uint64_t base) {
 #pragma unroll
@@ -842,17 +856,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
       base = tile_base(tile0 + tt + 1);
       prefetch(base);
     }
-    uint32_t gi_op = 0;
+    uint32_t ri = 0;  // reduction op index (accumulator slot)
     for (uint32_t j = 0; j < fg.nops; ++j) {
       const fop op = ops[j];
-      const uint32_t kind = op.kind & 3u;
-      const bool grad = TWO && (op.kind & 4u);
+      const uint32_t kind = op.kind & 7u;
+      const bool gamma = TWO && (op.kind & FOP_GAMMA);
       const cx* M = mats + op.mat;
-      if (kind == 0) {  // one-qubit dense
+      if (kind == FK_Q1 || kind == FK_DENS1 || kind == FK_INJ1) {  // pairs along t1
         cx A[4], B[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) A[i] = M[i];
-        if constexpr (TWO) {
+        if constexpr (TWO && WF) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
         }
@@ -862,9 +876,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           const uint32_t grp = t + it * BLOCK;
           const uint32_t a0 = swz((uint32_t)insert_zero(grp, op.t1));
           cx fx[2] = {lf[a0], lf[a0 ^ s1]};
+          if constexpr (!TWO) {
+            if (kind == FK_DENS1) {
+#pragma unroll
+              for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                  acc[p * 2 + q] = cfma_conj(fx[p], fx[q], acc[p * 2 + q]);
+              continue;
+            }
+          }
+          if constexpr (TWO && !WF) {  // injection-only pass: b += M (2 conj f)
+            const cx b0 = lb[a0], b1 = lb[a0 ^ s1];
+            cx tx[2] = {{2 * fx[0].x, -2 * fx[0].y}, {2 * fx[1].x, -2 * fx[1].y}};
+            umatvec<2>(A, tx);
+            lb[a0] = cadd(b0, tx[0]);
+            lb[a0 ^ s1] = cadd(b1, tx[1]);
+            continue;
+          }
           if constexpr (TWO) {
             cx bx[2] = {lb[a0], lb[a0 ^ s1]};
-            if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
+            if (gamma) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -880,20 +912,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           lf[a0] = fx[0];
           lf[a0 ^ s1] = fx[1];
         }
-        if (grad) {
-          real v[8];
+        if constexpr (HASRED) {
+          if (gamma || kind == FK_DENS1) {
+            real v[8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[2 * i] = acc[i].x;
-            v[2 * i + 1] = acc[i].y;
+            for (int i = 0; i < 4; ++i) {
+              v[2 * i] = acc[i].x;
+              v[2 * i + 1] = acc[i].y;
+            }
+            wave_reduce_add<8>(v, &accw[wave][ri][0]);
+            ++ri;
           }
-          wave_reduce_add<8>(v, &accw[wave][gi_op][0]);
         }
-      } else if (kind == 1) {  // two-qubit dense
+      } else if (kind == FK_Q2 || kind == FK_DENS2 || kind == FK_INJ2) {  // quartets
         cx A[16], B[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) A[i] = M[i];
-        if constexpr (TWO) {
+        if constexpr (TWO && WF) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
         }
@@ -910,10 +945,31 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
           cx fx[4], bx[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) fx[r] = lf[a0 ^ soff[r]];
+          if constexpr (!TWO) {
+            if (kind == FK_DENS2) {
+#pragma unroll
+              for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  acc[p * 4 + q] = cfma_conj(fx[p], fx[q], acc[p * 4 + q]);
+              continue;
+            }
+          }
+          if constexpr (TWO && !WF) {  // injection-only pass: b += M (2 conj f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              bx[r] = lb[a0 ^ soff[r]];
+              fx[r] = {2 * fx[r].x, -2 * fx[r].y};
+            }
+            umatvec<4>(A, fx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lb[a0 ^ soff[r]] = cadd(bx[r], fx[r]);
+            continue;
+          }
           if constexpr (TWO) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bx[r] = lb[a0 ^ soff[r]];
-            if (grad) {  // Gamma = sum b0 f0^T of the stage-entry states
+            if (gamma) {  // Gamma = sum b0 f0^T of the stage-entry states
 #pragma unroll
               for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -929,17 +985,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
 #pragma unroll
           for (int r = 0; r < 4; ++r) lf[a0 ^ soff[r]] = fx[r];
         }
-        if (grad) {
-          real v[32];
+        if constexpr (HASRED) {
+          if (gamma || kind == FK_DENS2) {
+            real v[32];
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            v[2 * i] = acc[i].x;
-            v[2 * i + 1] = acc[i].y;
+            for (int i = 0; i < 16; ++i) {
+              v[2 * i] = acc[i].x;
+              v[2 * i + 1] = acc[i].y;
+            }
+            wave_reduce_add<32>(v, &accw[wave][ri][0]);
+            ++ri;
           }
-          wave_reduce_add<32>(v, &accw[wave][gi_op][0]);
         }
-      } else {  // two-qubit diagonal: A = applied diagonal (uncompute: conj), B = d
-        // quartets over (pos2, pos1): element r = 2 P2 + P1 takes diagonal entry r (static)
+      } else if constexpr (!(TWO && !WF)) {  // diagonal stage: A applied, B pull-back
+        // quartets over (hi, lo): element r = 2 bit(hi) + bit(lo) takes diagonal entry r
         cx A[4], B[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) A[i] = M[i];
@@ -961,35 +1020,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED
             lf[a0 ^ soff[r]] = ucmul(A[r], f0);
             if constexpr (TWO) {
               const cx bv = lb[a0 ^ soff[r]];
-              if (grad) acc[r] = vcfma(bv, f0, acc[r]);
+              if (gamma) acc[r] = vcfma(bv, f0, acc[r]);
               lb[a0 ^ soff[r]] = ucmul(B[r], bv);
             }
           }
         }
-        if (grad) {
-          real v[8];
+        if constexpr (HASRED) {
+          if (gamma) {
+            real v[8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[2 * i] = acc[i].x;
-            v[2 * i + 1] = acc[i].y;
+            for (int i = 0; i < 4; ++i) {
+              v[2 * i] = acc[i].x;
+              v[2 * i + 1] = acc[i].y;
+            }
+            wave_reduce_add<8>(v, &accw[wave][ri][0]);
+            ++ri;
           }
-          wave_reduce_add<8>(v, &accw[wave][gi_op][0]);
         }
       }
-      gi_op += grad ? 1u : 0u;
       __syncthreads();
     }
     // each thread stores (and next refills) only its own chunks: no barrier needed here
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const uint32_t c = swz_chunk(t + (uint32_t)i * BLOCK);
-      stc(f + cur + off[i], lds[0][c]);
+      if constexpr (WF) stc(f + cur + off[i], lds[0][c]);
       if constexpr (TWO) stc(b + cur + off[i], lds[NS - 1][c]);
     }
     if (tt + 1 < count) fill();
   }
-  if constexpr (TWO) {
-    // one partial (16 complex) per block and gradient gate: slot k at partials + k*slot_stride
+  if constexpr (HASRED) {
+    // one partial (16 complex) per block and reduction op: slot k at partials + k*slot_stride
     for (uint32_t i = t; i < fg.ngrad * FACC; i += BLOCK) {
       const uint32_t k = i / FACC, e = i % FACC;
       real s = 0;

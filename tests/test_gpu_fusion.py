@@ -111,3 +111,69 @@ def test_fused_with_local_shards(shards):
     assert normrel(c.forward(const, var), dens) < 1e-10
     assert normrel(c.backward(cots, const, var), grads) < 1e-9
     assert normrel([c.get_state(0)], [final]) < 1e-9
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fused_densities_and_injections_order_rules(prec):
+    """Densities / cotangent injections inside fused passes: dense interleaving with
+    non-unitary and variable gates on other qubits (the ordering rules), plain densities in
+    run mode, and every density batched (no standalone density / injection launches when all
+    of them fit tiles)."""
+    dt = DT[prec]
+    n = 14
+    ins, const, var = O.random_circuit(n, 120, seed=321, density_every=3)
+    # plain densities too (run mode reports them)
+    ins = ins[:20] + [(O.Q1_DENSITY, (3,)), (O.Q2_DENSITY, (9, 2))] + ins[20:]
+    cg = [g.astype(dt) for g in const]
+    vg = [g.astype(dt) for g in var]
+    psi0 = O.random_state(np.random.default_rng(5), n).astype(dt)
+    o = O.OracleCircuit(n, dt)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    o.set_state_from_vector(psi0)
+    want_run = o.run(cg, vg)
+    dens, cots, grads, final = oracle_pass(n, ins, cg, vg, psi0, dt)
+    c = build(prec, n, ins, 1)
+    c.set_state_from_vector(psi0)
+    assert normrel(c.run(cg, vg), want_run) < TOL[prec]
+    assert normrel(c.forward(cg, vg), dens) < TOL[prec]
+    assert normrel(c.backward(cots, cg, vg), grads) < TOL[prec] * 10
+    assert normrel([c.get_state(0)], [final]) < TOL[prec] * 10
+
+
+def test_bench_circuit_batches_densities_and_injections():
+    import quantum_differentiable_circuit as q
+    n = 20
+    ins, var = O.layered_circuit(n, 2, seed=3)
+    vg = [g.astype(np.complex64) for g in var]
+    c = build("f32", n, ins, 1)
+    c.profile(True)
+    d = c.forward([], vg)
+    g = c.backward([np.diag([1.0, -1.0]).astype(np.complex64) for _ in d], [], vg)
+    stats = c.profile_collect()
+    assert not any(k.startswith(("density", "inject")) for k in stats), sorted(stats)
+    ref = build("f32", n, ins, 0)
+    d0 = ref.forward([], vg)
+    g0 = ref.backward([np.diag([1.0, -1.0]).astype(np.complex64) for _ in d0], [], vg)
+    assert normrel(d, d0) < 1e-5 and normrel(g, g0) < 1e-5
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fused_densities_with_nonunitary_matrices_on_unitary_kinds(prec):
+    """The reference applies whatever matrix a unitary-kind gate carries (the FD test perturbs
+    them); a density may only pass gates that are unitary to working precision, so fused
+    forward densities must still match the oracle exactly."""
+    dt = DT[prec]
+    n = 14
+    ins, const, var = O.random_circuit(n, 100, seed=77, density_every=2)
+    rng = np.random.default_rng(8)
+    var = [g + 1e-3 * (rng.standard_normal(g.shape) + 1j * rng.standard_normal(g.shape))
+           for g in var]
+    cg = [g.astype(dt) for g in const]
+    vg = [np.ascontiguousarray(g, dtype=dt) for g in var]
+    o = O.OracleCircuit(n, dt)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    want = o.forward(cg, vg)
+    c = build(prec, n, ins, 1)
+    assert normrel(c.forward(cg, vg), want) < TOL[prec] / 10

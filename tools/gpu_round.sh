@@ -16,10 +16,10 @@ timeout -k 10 900 python bench.py > "$OUT/bench.log" 2>&1 || exit $?
 tail -c 600 "$OUT/bench.log"; echo
 step rocprof-kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace \
-  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/trace.log" 2>&1 || exit $?
+  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-gate-sample > "$OUT/trace.log" 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
   step "pmc $c"
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o pmc \
-    -- python3 bench.py --steps 1 --warmup 0 --layers 2 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1 || exit $?
+    -- python3 bench.py --steps 1 --warmup 0 --layers 2 --no-cpu-baseline --no-gate-sample > "$OUT/pmc_$c.log" 2>&1 || exit $?
 done
 step done
