@@ -869,7 +869,9 @@ struct Circuit {
     const double S = state_bytes(nl);
     const double bytes = two ? (it.writes_f ? 4.0 : 3.0) * S : (it.writes_f ? 2.0 : 1.0) * S;
     const double flops = it.flops_per_amp * (double)((uint64_t)1 << nl);
-    const char* name = two ? "fused_reverse" : "fused_apply";
+    // one name per kernel variant (bytes per launch differ: 4S, 3S, 2S, S)
+    const char* name = two ? (it.writes_f ? "fused_reverse" : "fused_inject")
+                           : (it.writes_f ? "fused_apply" : "fused_density");
     if (fg.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     for (auto& s : sh) {
       chunk* f = reinterpret_cast<chunk*>(s.state);

@@ -30,10 +30,11 @@ def bench_name(kernel):
     m = re.search(r"k_diag<(\d+)", kernel)
     if m:
         return DIAG[int(m.group(1))]
-    if "k_fused<false" in kernel:
-        return "fused_apply"
-    if "k_fused<true" in kernel:
-        return "fused_reverse"
+    m = re.search(r"k_fused<(true|false), \d+, (true|false), (true|false)>", kernel)
+    if m:  # <TWO, TB, HASRED, WF> -> the bench's per-variant names
+        two, wf = m.group(1) == "true", m.group(3) == "true"
+        return ("fused_reverse" if wf else "fused_inject") if two else \
+               ("fused_apply" if wf else "fused_density")
     if "k_elementwise<0>" in kernel:
         return "copy"
     if "k_finalize" in kernel:
