@@ -241,3 +241,46 @@ QDC_API const char* qdc_build_info(void) {
   return "qdc f32 gfx950";
 #endif
 }
+
+QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t first_inject,
+                                   const int* kinds, const unsigned char* inexact,
+                                   size_t n_instr, const qdc_plan_op* plan, size_t n_plan,
+                                   int lcmin, int max_ops, unsigned* item_info, size_t item_cap,
+                                   unsigned* stage_len, size_t stage_cap, unsigned* op_order,
+                                   size_t op_cap) {
+  std::vector<qdc::Instr> ins(n_instr);
+  for (size_t k = 0; k < n_instr; ++k) ins[k] = qdc::Instr{kinds[k], 0, 0};
+  std::vector<uint8_t> sens(n_instr, 0);
+  if (inexact)
+    for (size_t k = 0; k < n_instr; ++k) sens[k] = inexact[k] ? 1 : 0;
+  const qdc::FusionPlanner P{ins, sens, (uint32_t)local_qubits, true, true,
+                             max_ops > 0 ? (uint32_t)std::min(max_ops, qdc::FMAX_OPS)
+                                         : (uint32_t)qdc::FMAX_OPS,
+                             lcmin > 0 ? (uint32_t)lcmin : 3u};
+  const std::vector<qdc_plan_op> pl(plan, plan + n_plan);
+  const std::vector<qdc::FusionItem> items = P.fuse_items(pl, backward != 0, first_inject);
+  size_t ns = 0, no = 0;
+  for (size_t i = 0; i < items.size(); ++i) {
+    const qdc::FusionItem& it = items[i];
+    std::vector<std::vector<uint32_t>> stages;
+    if (it.type == 2)
+      stages = P.stage_partition(it.ops, pl, backward != 0);
+    else
+      stages.push_back(it.ops);
+    if (i >= item_cap || ns + stages.size() > stage_cap) return SIZE_MAX;
+    unsigned* info = item_info + 12 * i;
+    info[0] = (unsigned)it.type;
+    info[1] = (unsigned)stages.size();
+    info[2] = it.lc;
+    info[3] = it.h;
+    for (int k = 0; k < 8; ++k) info[4 + k] = k < (int)qdc::FMAX_ROWS ? it.hb[k] : 0u;
+    for (const auto& st : stages) {
+      stage_len[ns++] = (unsigned)st.size();
+      for (uint32_t op : st) {
+        if (no >= op_cap) return SIZE_MAX;
+        op_order[no++] = op;
+      }
+    }
+  }
+  return items.size();
+}

@@ -18,43 +18,9 @@
 #include "qdc_device.hpp"
 #include "qdc_shard.hpp"
 #include "qdc_stage.hpp"
+#include "qdc_fusion.hpp"
 
 namespace qdc {
-
-struct Instr {
-  int kind;
-  uint32_t a;  // q1: pos; q2: pos2
-  uint32_t b;  // q2: pos1
-};
-
-inline bool is_q1_gate(int k) {
-  return k == QDC_CONST_Q1 || k == QDC_CONST_Q1_NONU || k == QDC_VAR_Q1 || k == QDC_VAR_Q1_NONU;
-}
-inline bool is_q2_dense(int k) {
-  return k == QDC_CONST_Q2 || k == QDC_VAR_Q2 || k == QDC_CONST_Q2_NONU || k == QDC_VAR_Q2_NONU;
-}
-inline bool is_diag(int k) { return k == QDC_CONST_Q2_DIAG || k == QDC_VAR_Q2_DIAG; }
-inline bool is_const(int k) {
-  return k == QDC_CONST_Q1 || k == QDC_CONST_Q1_NONU || k == QDC_CONST_Q2 ||
-         k == QDC_CONST_Q2_NONU || k == QDC_CONST_Q2_DIAG;
-}
-inline bool is_var(int k) {
-  return k == QDC_VAR_Q1 || k == QDC_VAR_Q1_NONU || k == QDC_VAR_Q2 || k == QDC_VAR_Q2_NONU ||
-         k == QDC_VAR_Q2_DIAG;
-}
-inline bool is_nonu(int k) {
-  return k == QDC_CONST_Q1_NONU || k == QDC_VAR_Q1_NONU || k == QDC_CONST_Q2_NONU ||
-         k == QDC_VAR_Q2_NONU;
-}
-inline bool is_density(int k) {
-  return k == QDC_Q1_DENSITY || k == QDC_Q2_DENSITY || k == QDC_DIFF_Q1_DENSITY ||
-         k == QDC_DIFF_Q2_DENSITY;
-}
-inline bool is_diff_density(int k) {
-  return k == QDC_DIFF_Q1_DENSITY || k == QDC_DIFF_Q2_DENSITY;
-}
-inline bool is_q1_density(int k) { return k == QDC_Q1_DENSITY || k == QDC_DIFF_Q1_DENSITY; }
-inline int gate_len(int k) { return is_q2_dense(k) ? 16 : 4; }
 
 // A flattened list of host buffers (gate matrices or density cotangents).
 struct Flat {
@@ -180,9 +146,11 @@ struct Circuit {
   uint32_t fuse_max_ops = FMAX_OPS;
   uint32_t fuse_lcmin = 3;  // min contiguous chunk bits of a fused tile (128-B rows)
   int fuse_meas = 1;        // densities / cotangent injections join fused passes
-  std::vector<uint8_t> fwd_sens;  // per instruction: gate not unitary to working precision
+  std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
-  uint32_t fused_resident[2] = {0, 0};
+  std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
+  int fused_nt1 = 256, fused_nt2 = 256;  // threads per block of one- / two-state passes
+  uint32_t last_fused_grid = 0;
   unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
   unsigned char* prog_host = nullptr;  // pinned staging
   std::vector<StagePost> stage_post;   // gradient recipes of the last backward's stages
@@ -207,6 +175,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
       fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
     if (const char* e = getenv("QDC_FUSE_MEAS")) fuse_meas = atoi(e);
+    if (const char* e = getenv("QDC_FUSED_NT1")) fused_nt1 = atoi(e) == 128 ? 128 : 256;
+    if (const char* e = getenv("QDC_FUSED_NT2")) fused_nt2 = atoi(e) == 128 ? 128 : 256;
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
@@ -396,81 +366,44 @@ struct Circuit {
     return out;
   }
 
-  // --- fusion: gates whose qubits fit one tile run as one HBM pass ---------------------------
-  // Gates on disjoint qubits commute, so within a segment of consecutive gate ops (bounded by
-  // remaps, densities and cotangent injections) a pass may take any gate none of whose
-  // earlier same-qubit gates is left for a later pass.  Each pass is built greedily in
-  // program order: a gate joins if it is ready and its qubits still fit the tile, otherwise
-  // its qubits are blocked for the rest of the scan.  Per qubit, gates keep program order, so
-  // the result equals the sequential one up to floating-point rounding.
-  struct Item {
-    int type;                    // 0: one plan op, 1: remap, 2: fused group
-    std::vector<uint32_t> ops;   // plan indices (one for type 0/1), program order
-    uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {};
+  struct Item : FusionItem {
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t nstage = 0;  // fop count (stages) of the pass
     double flops_per_amp = 0;  // algorithmic real FLOPs per amplitude of the pass
     bool has_red = false;      // reduction ops (Gamma stages or densities)
     bool writes_f = false;     // gate stages (fwd changes; else fwd is only read)
-    uint32_t ngrad = 0;
     std::vector<uint32_t> grad_slots;  // reduction slot of each reduction op, in op order
   };
-  static constexpr uint32_t TILE_CHUNKS_1 = 2048;  // one-state fused tile (chunks)
-  static constexpr uint32_t TILE_CHUNKS_2 = 1024;  // two-state fused tile (chunks per state)
-
-  uint64_t chunk_bits_of(uint32_t p) const { return p >= (uint32_t)LV ? 1ull << (p - LV) : 0ull; }
-  // A full tile of 2^T chunks: lc contiguous chunk bits (>= fuse_lcmin) plus h = T - lc row
-  // bits that cover the group's far target bits, padded with the lowest free bits above lc.
-  // States with fewer than 2^T chunks are not fused.
-  bool tile_config(uint64_t mask, uint32_t T, uint32_t& lc, uint32_t& h, uint32_t* hb) const {
-    const uint32_t cbits = nl - LV;
-    if (cbits < T) return false;
-    for (int l = (int)T; l >= (int)fuse_lcmin; --l) {
-      uint32_t rows = 0, tmp[64];
-      for (uint32_t c = (uint32_t)l; c < cbits; ++c)
-        if (mask >> c & 1ull) tmp[rows++] = c;
-      if (rows > (uint32_t)FMAX_ROWS || (uint32_t)l + rows > T) continue;
-      for (uint32_t c = (uint32_t)l; c < cbits && (uint32_t)l + rows < T; ++c)
-        if (!(mask >> c & 1ull)) tmp[rows++] = c;
-      if ((uint32_t)l + rows != T || rows > (uint32_t)FMAX_ROWS) continue;
-      std::sort(tmp, tmp + rows);
-      lc = (uint32_t)l;
-      h = rows;
-      for (uint32_t k = 0; k < rows; ++k) hb[k] = tmp[k];
-      return true;
+  static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
+  static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
+  FusionPlanner planner() const {
+    return FusionPlanner{ins, inexact, nl, fuse != 0, fuse_meas != 0, fuse_max_ops, fuse_lcmin};
+  }
+  bool is_meas(const qdc_plan_op& op) const { return planner().is_meas(op); }
+  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
+                               size_t first_inject = SIZE_MAX) const {
+    std::vector<Item> items;
+    for (FusionItem& f : planner().fuse_items(plan, backward, first_inject)) {
+      Item it;
+      static_cast<FusionItem&>(it) = std::move(f);
+      items.push_back(std::move(it));
     }
-    return false;
+    return items;
   }
-  bool tile_fits(uint64_t mask, uint32_t T) const {
-    if (nl - LV < T) return false;
-    for (int l = (int)T; l >= (int)fuse_lcmin; --l) {
-      const uint32_t rows = (uint32_t)__builtin_popcountll(mask >> l);
-      if (rows <= (uint32_t)FMAX_ROWS && (uint32_t)l + rows <= T) return true;
-    }
-    return false;
+  std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
+                                                     const std::vector<qdc_plan_op>& plan,
+                                                     bool backward) const {
+    return planner().stage_partition(pass, plan, backward);
   }
-
-  // Ordering rules beyond "same qubit => program order" (qdc_stage.hpp has the algebra):
-  //  * a density commutes with unitary gates on other qubits, not with non-unitary ones;
-  //  * a cotangent injection (reverse sweep) commutes only with const unitary gates on other
-  //    qubits: a variable gate's gradient sees the bwd state, so it keeps its order.
-  // "meas" ops (densities, injections) and "sensitive" gates (non-unitary; in the reverse
-  // sweep also variable) therefore never pass each other: once one kind is left for a later
-  // pass or stage, every later op of the other kind is too.
-  bool is_meas(const qdc_plan_op& op) const {
-    return op.type == QDC_PLAN_OP && is_density(ins[op.instr].kind);
-  }
-  // Forward: a density passes a gate on other qubits only if the gate is unitary to
-  // working precision (the reduced density is invariant under U_B only if U_B^+ U_B = I), so
-  // it is checked per call on the actual matrices (fwd_sens).  Reverse sweep: the reference
-  // uncomputes every non-NonU kind with U^+ (diagonal: conj), so B = U^T = conj(A) holds by
-  // construction and an injection commutes with such const gates whatever the matrix.
-  bool is_sens(const qdc_plan_op& op, bool backward) const {
-    if (op.type != QDC_PLAN_OP) return false;
-    const int k = ins[op.instr].kind;
-    if (!(is_const(k) || is_var(k))) return false;
-    if (backward) return is_nonu(k) || is_var(k);
-    return is_nonu(k) || (op.instr < fwd_sens.size() && fwd_sens[op.instr]);
+  // per call: which gates are not unitary to working precision (qdc_fusion.hpp)
+  void mark_inexact(const Flat& cg, const Flat& vg, const std::vector<size_t>& gidx) {
+    inexact.assign(ins.size(), 0);
+    const double utol = sizeof(real) == 4 ? 1e-6 : 1e-13;
+    for (size_t k = 0; k < ins.size(); ++k)
+      if (is_const(ins[k].kind) || is_var(ins[k].kind)) {
+        const qdc_complex* g4 = is_const(ins[k].kind) ? cg.at(gidx[k]) : vg.at(gidx[k]);
+        inexact[k] = unitarity_error(g4, ins[k].kind) > utol ? 1 : 0;
+      }
   }
   // max |U^+ U - I| of a gate's host matrix (diagonal: max ||d_i|^2 - 1|)
   static double unitarity_error(const qdc_complex* g, int kind) {
@@ -496,141 +429,6 @@ struct Circuit {
       }
     return e;
   }
-  bool is_gate_op(const qdc_plan_op& op) const {
-    if (op.type != QDC_PLAN_OP) return false;
-    const int k = ins[op.instr].kind;
-    return is_const(k) || is_var(k);
-  }
-  uint64_t op_bits(const qdc_plan_op& op) const {
-    return chunk_bits_of(op.pos2) | chunk_bits_of(op.pos1);
-  }
-
-  // backward: plan indices >= first_inject run two-state (bwd exists); a pass never spans it.
-  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
-                               size_t first_inject = SIZE_MAX) const {
-    std::vector<Item> items;
-    const uint32_t T = log2u(backward ? TILE_CHUNKS_2 : TILE_CHUNKS_1);
-    const bool on = fuse && fuse_max_ops >= 2;
-    auto fusable = [&](size_t k) {
-      const qdc_plan_op& op = plan[k];
-      if (!(is_gate_op(op) || (fuse_meas && is_meas(op))) || !tile_fits(op_bits(op), T))
-        return false;
-      // injections need bwd: only in the two-state part
-      return !(backward && is_meas(op) && k < first_inject);
-    };
-    size_t i = 0;
-    while (i < plan.size()) {
-      const qdc_plan_op& op = plan[i];
-      if (op.type == QDC_PLAN_REMAP) {
-        items.push_back(Item{1, {(uint32_t)i}});
-        ++i;
-        continue;
-      }
-      if (!on || !fusable(i)) {
-        items.push_back(Item{0, {(uint32_t)i}});
-        ++i;
-        continue;
-      }
-      size_t j = i;
-      while (j < plan.size() && plan[j].type == QDC_PLAN_OP && fusable(j) &&
-             !(backward && j == first_inject && j > i))
-        ++j;
-      const bool two = backward && i >= first_inject;
-      std::vector<uint32_t> rem;
-      for (size_t k = i; k < j; ++k) rem.push_back((uint32_t)k);
-      while (!rem.empty()) {
-        uint64_t mask = 0, blocked = 0;
-        uint32_t nred = 0;
-        bool meas_left = false, sens_left = false;
-        std::vector<uint32_t> pass, rest;
-        int kind = -1;  // reverse sweep: a pass is injections only or gates only
-        for (uint32_t k : rem) {
-          const qdc_plan_op& g = plan[k];
-          const uint64_t q = (1ull << g.pos2) | (1ull << g.pos1);
-          const bool meas = is_meas(g), sens = is_sens(g, backward);
-          if (backward && kind >= 0 && (int)meas != kind) {
-            blocked |= q;
-            meas_left = meas_left || meas;
-            sens_left = sens_left || sens;
-            rest.push_back(k);
-            continue;
-          }
-          const uint32_t isred =
-              ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
-          if ((q & blocked) || (meas && sens_left) || (sens && meas_left) ||
-              pass.size() >= fuse_max_ops || nred + isred > (uint32_t)FMAX_GRAD ||
-              !tile_fits(mask | op_bits(g), T)) {
-            blocked |= q;
-            meas_left = meas_left || meas;
-            sens_left = sens_left || sens;
-            rest.push_back(k);
-            continue;
-          }
-          pass.push_back(k);
-          mask |= op_bits(g);
-          nred += isred;
-          kind = (int)meas;
-        }
-        if (pass.size() == 1) {
-          items.push_back(Item{0, pass});
-        } else {
-          Item it{2, pass};
-          tile_config(mask, T, it.lc, it.h, it.hb);
-          items.push_back(it);
-        }
-        rem.swap(rest);
-      }
-      i = j;
-    }
-    return items;
-  }
-
-  // Split a pass (plan indices in pass order) into stages: greedy in program order, a gate
-  // joins the current stage if none of its qubits is blocked (an earlier gate on it is left
-  // for a later stage) and the stage stays within two qubits.  Per qubit, order is kept.
-  std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
-                                                     const std::vector<qdc_plan_op>& plan,
-                                                     bool backward) const {
-    std::vector<std::vector<uint32_t>> stages;
-    std::vector<uint32_t> rem = pass;
-    while (!rem.empty()) {
-      std::vector<uint32_t> st, rest;
-      uint64_t q = 0, blocked = 0;
-      bool meas_left = false, sens_left = false, closed = false;
-      for (uint32_t k : rem) {
-        if (closed) {
-          rest.push_back(k);
-          continue;
-        }
-        const qdc_plan_op& g = plan[k];
-        const uint64_t gq = (1ull << g.pos2) | (1ull << g.pos1);
-        const bool meas = is_meas(g), sens = is_sens(g, backward);
-        bool bad = (gq & blocked) || (meas && sens_left) || (sens && meas_left);
-        if (!bad && meas) {
-          if (st.empty()) {  // a density / injection is a stage of its own
-            st.push_back(k);
-            closed = true;
-            continue;
-          }
-          bad = true;
-        }
-        if (!bad && __builtin_popcountll(q | gq) > 2) bad = true;
-        if (bad) {
-          blocked |= gq;
-          meas_left = meas_left || meas;
-          sens_left = sens_left || sens;
-          rest.push_back(k);
-          continue;
-        }
-        st.push_back(k);
-        q |= gq;
-      }
-      stages.push_back(std::move(st));
-      rem.swap(rest);
-    }
-    return stages;
-  }
-
   // Lay out every fused pass's stage descriptors and stage matrices (A = product of the
   // applied matrices, B = product of the bwd pull-backs) in one pinned buffer, then upload it.
   // backward: `first_inject` = plan index of the first cotangent injection (passes before it
@@ -812,7 +610,6 @@ struct Circuit {
           stage_post.push_back(std::move(post));
         }
       }
-      it.ngrad = (uint32_t)it.grad_slots.size();
       it.nstage = (uint32_t)stages_of[ii].size();
     }
     QDC_HIP(hipMemcpyAsync(prog_dev, prog_host, mats_off + mo * sizeof(cx),
@@ -822,13 +619,51 @@ struct Circuit {
 
   // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
   // gradient gates write partials for gradient buffer rows var_idx[...].
-  template <bool TWO, bool HASRED, bool WF>
-  const char* launch_fused(const char* name, double bytes, uint32_t grid, chunk* f, chunk* b,
-                           const fop* fops, const cx* mats, const fgeo& fg, cx* partials,
-                           uint64_t stride) {
+  template <bool TWO, bool HASRED, bool WF, int NT>
+  static auto fused_kernel() {
     constexpr int TB = TWO ? (int)TILE_CHUNKS_2 : (int)TILE_CHUNKS_1;
-    return ctx.launch(name, bytes, k_fused<TWO, TB, HASRED, WF>, grid, f, b, fops, mats, fg,
-                      partials, stride);
+    return k_fused<TWO, TB, HASRED, WF, NT>;
+  }
+  template <bool TWO, bool HASRED, bool WF>
+  const char* launch_fused(const char* name, double bytes, const fgeo& fg, chunk* f, chunk* b,
+                           const fop* fops, const cx* mats, cx* partials, uint64_t stride) {
+    const int nt = TWO ? fused_nt2 : fused_nt1;
+    uint32_t grid = 0;
+    QDC_TRY(fused_grid(fg, nt == 128 ? (const void*)fused_kernel<TWO, HASRED, WF, 128>()
+                                     : (const void*)fused_kernel<TWO, HASRED, WF, 256>(),
+                       nt, grid));
+    fgeo g = fg;
+    uint64_t tpb = 1;
+    while (tpb * grid < g.ntiles) tpb <<= 1;
+    g.tpb = (uint32_t)tpb;
+    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
+    last_fused_grid = grid;
+    if (nt == 128)
+      return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, 128>(), grid, 128u, f, b,
+                              fops, mats, g, partials, stride);
+    return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, 256>(), grid, 256u, f, b,
+                            fops, mats, g, partials, stride);
+  }
+  // one wave of resident blocks (occupancy query, cached per kernel), or QDC_FUSED_BLOCKS
+  const char* fused_grid(const fgeo& fg, const void* kernel, int nt, uint32_t& grid) {
+    if (fused_blocks) {
+      grid = fused_blocks;
+      return nullptr;
+    }
+    for (auto& e : fused_resident_cache)
+      if (e.first == kernel) {
+        grid = e.second;
+        return nullptr;
+      }
+    int per_cu = 0, dev = 0, cus = 0;
+    QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, nt, 0));
+    QDC_HIP(hipGetDevice(&dev));
+    QDC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    grid = (uint32_t)std::max(1, std::min(per_cu * cus, (int)NBMAX));
+    fused_resident_cache.push_back({kernel, grid});
+    (void)fg;
+    return nullptr;
   }
 
   // Run one fused pass on every shard.  two: fwd and bwd (reverse sweep).  Reductions (Gamma
@@ -841,28 +676,6 @@ struct Circuit {
     fg.nops = it.nstage;
     fg.ngrad = it.has_red ? (uint32_t)it.grad_slots.size() : 0;
     fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
-    // one wave of resident blocks, each pipelining a contiguous run of tiles
-    uint32_t target = fused_blocks;
-    if (target == 0) {
-      uint32_t& res = fused_resident[two ? 1 : 0];
-      if (res == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (two)
-          QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, k_fused<true, TILE_CHUNKS_2, true, true>, BLOCK, 0));
-        else
-          QDC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &per_cu, k_fused<false, TILE_CHUNKS_1, true, true>, BLOCK, 0));
-        QDC_HIP(hipGetDevice(&dev));
-        QDC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        res = (uint32_t)std::max(1, std::min(per_cu * cus, (int)NBMAX));
-      }
-      target = res;
-    }
-    uint64_t tpb = 1;
-    while (tpb * target < fg.ntiles) tpb <<= 1;
-    fg.tpb = (uint32_t)tpb;
-    const uint32_t grid = (uint32_t)((fg.ntiles + tpb - 1) / tpb);
     const fop* fops = reinterpret_cast<const fop*>(prog_dev + it.fop_off);
     const cx* mats = reinterpret_cast<const cx*>(prog_dev + mats_off);
     // algorithmic bytes: each state read once, written once if the pass changes it
@@ -872,7 +685,6 @@ struct Circuit {
     // one name per kernel variant (bytes per launch differ: 4S, 3S, 2S, S)
     const char* name = two ? (it.writes_f ? "fused_reverse" : "fused_inject")
                            : (it.writes_f ? "fused_apply" : "fused_density");
-    if (fg.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     for (auto& s : sh) {
       chunk* f = reinterpret_cast<chunk*>(s.state);
       chunk* b = reinterpret_cast<chunk*>(s.bwd);
@@ -889,23 +701,18 @@ struct Circuit {
       ctx.next_flops = flops;
       if (two) {
         if (it.writes_f)
-          QDC_TRY((launch_fused<true, true, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
-                                                   stride)));
+          QDC_TRY((launch_fused<true, true, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
         else
-          QDC_TRY((launch_fused<true, false, false>(name, bytes, grid, f, b, fops, mats, fg,
-                                                     parts, stride)));
+          QDC_TRY((launch_fused<true, false, false>(name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else if (!it.has_red) {
-        QDC_TRY((launch_fused<false, false, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
-                                                   stride)));
+        QDC_TRY((launch_fused<false, false, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else if (it.writes_f) {
-        QDC_TRY((launch_fused<false, true, true>(name, bytes, grid, f, b, fops, mats, fg, parts,
-                                                  stride)));
+        QDC_TRY((launch_fused<false, true, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else {
-        QDC_TRY((launch_fused<false, true, false>(name, bytes, grid, f, b, fops, mats, fg, parts,
-                                                   stride)));
+        QDC_TRY((launch_fused<false, true, false>(name, bytes, fg, f, b, fops, mats, parts, stride)));
       }
       if (fg.ngrad > 0)
-        for (uint32_t slot : it.grad_slots) ctx.commit(slot, grid);
+        for (uint32_t slot : it.grad_slots) ctx.commit(slot, last_fused_grid);
     }
     return nullptr;
   }
@@ -956,13 +763,7 @@ struct Circuit {
           out_idx[k] = o++;
     }
     const std::vector<qdc_plan_op> pl = plan(mode);
-    fwd_sens.assign(ins.size(), 0);
-    const double utol = sizeof(real) == 4 ? 1e-6 : 1e-13;
-    for (size_t k = 0; k < ins.size(); ++k)
-      if (is_const(ins[k].kind) || is_var(ins[k].kind)) {
-        const qdc_complex* g4 = is_const(ins[k].kind) ? cg.at(gidx[k]) : vg.at(gidx[k]);
-        fwd_sens[k] = unitarity_error(g4, ins[k].kind) > utol ? 1 : 0;
-      }
+    mark_inexact(cg, vg, gidx);
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
@@ -1051,6 +852,7 @@ struct Circuit {
         first_inject = i;
         break;
       }
+    mark_inexact(cg, vg, gidx);
     std::vector<Item> items = fuse_items(pl, true, first_inject);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,

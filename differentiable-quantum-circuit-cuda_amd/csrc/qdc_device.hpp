@@ -135,13 +135,18 @@ struct Ctx {
 
   template <typename K, typename... Args>
   const char* launch(const char* name, double bytes, K kernel, uint32_t grid, Args... args) {
+    return launch_block(name, bytes, kernel, grid, (uint32_t)BLOCK, args...);
+  }
+  template <typename K, typename... Args>
+  const char* launch_block(const char* name, double bytes, K kernel, uint32_t grid,
+                           uint32_t block, Args... args) {
     hipEvent_t a = nullptr, b = nullptr;
     if (prof.on) {
       a = prof.get();
       b = prof.get();
       if (a) (void)hipEventRecord(a, stream);
     }
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(BLOCK), 0, stream, args...);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, stream, args...);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
       return fail("HIP ERROR: launch of kernel %s failed with %s.", name, hipGetErrorName(e));

@@ -615,10 +615,17 @@ __device__ __forceinline__ cx vcfma(cx a, cx f, cx c) {  // c + a f, both per la
   const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
   return __builtin_bit_cast(cx, vpk_im_fma(A, F, vpk_re_fma(A, F, __builtin_bit_cast(pk2, c))));
 }
+__device__ __forceinline__ cx vcmul(cx a, cx f) {  // a f, both per lane
+  const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
+  pk2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(A), "v"(F));
+  return __builtin_bit_cast(cx, vpk_im_fma(A, F, r));
+}
 #else
 __device__ __forceinline__ cx ucfma(cx a, cx f, cx c) { return cfma(a, f, c); }
 __device__ __forceinline__ cx ucmul(cx a, cx f) { return cmul(a, f); }
 __device__ __forceinline__ cx vcfma(cx a, cx f, cx c) { return cfma(a, f, c); }
+__device__ __forceinline__ cx vcmul(cx a, cx f) { return cmul(a, f); }
 #endif
 
 // x <- M x with a wave-uniform M (row-major R x R)
@@ -783,20 +790,22 @@ constexpr uint32_t FOP_GAMMA = 8;  // stage also accumulates Gamma = sum b0 f0^T
 // TWO: the pass carries fwd and bwd (reverse sweep); HASRED: the pass has reduction ops (Gamma,
 // densities) and their LDS accumulators; WF: the pass changes fwd, so fwd is stored back
 // (density-only and injection-only passes read it only).
-template <bool TWO, int TB, bool HASRED, bool WF>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(QDC_FUSED_WAVES)))
+// NT: threads per block (a tile of TB chunks is NT threads' work: fewer threads = more
+// quartets per thread per stage, amortising the per-stage reduce and setup).
+template <bool TWO, int TB, bool HASRED, bool WF, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? QDC_FUSED_WAVES : 2)))
 void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
              const cx* __restrict__ mats, fgeo fg, cx* __restrict__ partials,
              uint64_t slot_stride) {
   constexpr int NS = TWO ? 2 : 1;
-  constexpr int CPT = TB / BLOCK;  // chunks of each state per thread and tile
-  static_assert(TB % BLOCK == 0 && TB * VEC >= 4 * BLOCK, "tile must cover the block");
+  constexpr int CPT = TB / NT;  // chunks of each state per thread and tile
+  static_assert(TB % NT == 0 && TB * VEC >= 4 * NT, "tile must cover the block");
   __shared__ chunk lds[NS][TB];
-  __shared__ real accw[HASRED ? BLOCK / 64 : 1][HASRED ? FMAX_GRAD : 1][FACC];
+  __shared__ real accw[HASRED ? NT / 64 : 1][HASRED ? FMAX_GRAD : 1][FACC];
   const uint32_t t = threadIdx.x;
   const int wave = t >> 6;
   if constexpr (HASRED) {
-    for (uint32_t i = t; i < (BLOCK / 64) * FMAX_GRAD * FACC; i += BLOCK)
+    for (uint32_t i = t; i < (NT / 64) * FMAX_GRAD * FACC; i += NT)
       (&accw[0][0][0])[i] = 0;
   }
   // a tile is always TB chunks (lc + h == log2 TB; the host fuses nothing in smaller states),
@@ -804,11 +813,11 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
   constexpr uint32_t ta = TB * VEC;  // amplitudes per tile
   cx* lf = reinterpret_cast<cx*>(&lds[0][0]);
   cx* lb = reinterpret_cast<cx*>(&lds[NS - 1][0]);
-  // thread-owned tile chunks c = t + i*BLOCK sit at the same offset from every tile's base
+  // thread-owned tile chunks c = t + i*NT sit at the same offset from every tile's base
   uint64_t off[CPT];
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    const uint32_t c = t + (uint32_t)i * BLOCK;
+    const uint32_t c = t + (uint32_t)i * NT;
     uint64_t o = c & ((1u << fg.lc) - 1u);
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
@@ -837,7 +846,7 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
   auto fill = [&]() {  // pf -> LDS, each thread its own chunks
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const uint32_t c = swz_chunk(t + (uint32_t)i * BLOCK);
+      const uint32_t c = swz_chunk(t + (uint32_t)i * NT);
       lds[0][c] = pf[0][i];
       if constexpr (TWO) lds[NS - 1][c] = pf[NS - 1][i];
     }
@@ -872,9 +881,10 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
         }
         cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         const uint32_t s1 = swz(1u << op.t1);
-        for (uint32_t it = 0; it < ta / (2 * BLOCK); ++it) {
-          const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = swz((uint32_t)insert_zero(grp, op.t1));
+        const uint32_t abase = swz((uint32_t)insert_zero(t, op.t1));
+#pragma unroll
+        for (uint32_t it = 0; it < ta / (2 * NT); ++it) {
+          const uint32_t a0 = abase ^ swz((uint32_t)insert_zero(it * NT, op.t1));
           cx fx[2] = {lf[a0], lf[a0 ^ s1]};
           if constexpr (!TWO) {
             if (kind == FK_DENS1) {
@@ -932,16 +942,24 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
 #pragma unroll
           for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
         }
+        // with several quartets per thread (NT = 128) a Gamma stage seeds acc with its first
+        // product instead of zeroing it; at NT = 256 that lengthens live ranges into spills
+        constexpr bool SEED = NT == 128;
         cx acc[16];
+        if (!(SEED && gamma)) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = {0, 0};
+          for (int i = 0; i < 16; ++i) acc[i] = {0, 0};
+        }
         const uint32_t lo = op.t1 < op.t2 ? op.t1 : op.t2;
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
         const uint32_t s1 = swz(1u << op.t1), s2 = swz(1u << op.t2);
         const uint32_t soff[4] = {0, s1, s2, s1 ^ s2};
-        for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
-          const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = swz((uint32_t)insert_zero(insert_zero(grp, lo), hi));
+        // insert_zero and swz are linear over disjoint bits: quartet it of this thread sits at
+        // the thread's base XOR a uniform offset
+        const uint32_t abase = swz((uint32_t)insert_zero(insert_zero(t, lo), hi));
+#pragma unroll
+        for (uint32_t it = 0; it < ta / (4 * NT); ++it) {
+          const uint32_t a0 = abase ^ swz((uint32_t)insert_zero(insert_zero(it * NT, lo), hi));
           cx fx[4], bx[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) fx[r] = lf[a0 ^ soff[r]];
@@ -973,7 +991,9 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
 #pragma unroll
               for (int p = 0; p < 4; ++p)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc[p * 4 + q] = vcfma(bx[p], fx[q], acc[p * 4 + q]);
+                for (int q = 0; q < 4; ++q)
+                  acc[p * 4 + q] = (SEED && it == 0) ? vcmul(bx[p], fx[q])
+                                                     : vcfma(bx[p], fx[q], acc[p * 4 + q]);
             }
             umatvec<4>(A, fx);
             umatvec<4>(B, bx);
@@ -1011,9 +1031,10 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
         const uint32_t hi = op.t1 < op.t2 ? op.t2 : op.t1;
         const uint32_t s1 = swz(1u << op.t1), s2 = swz(1u << op.t2);
         const uint32_t soff[4] = {0, s1, s2, s1 ^ s2};
-        for (uint32_t it = 0; it < ta / (4 * BLOCK); ++it) {
-          const uint32_t grp = t + it * BLOCK;
-          const uint32_t a0 = swz((uint32_t)insert_zero(insert_zero(grp, lo), hi));
+        const uint32_t abase = swz((uint32_t)insert_zero(insert_zero(t, lo), hi));
+#pragma unroll
+        for (uint32_t it = 0; it < ta / (4 * NT); ++it) {
+          const uint32_t a0 = abase ^ swz((uint32_t)insert_zero(insert_zero(it * NT, lo), hi));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const cx f0 = lf[a0 ^ soff[r]];
@@ -1043,7 +1064,7 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
     // each thread stores (and next refills) only its own chunks: no barrier needed here
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const uint32_t c = swz_chunk(t + (uint32_t)i * BLOCK);
+      const uint32_t c = swz_chunk(t + (uint32_t)i * NT);
       if constexpr (WF) stc(f + cur + off[i], lds[0][c]);
       if constexpr (TWO) stc(b + cur + off[i], lds[NS - 1][c]);
     }
@@ -1051,11 +1072,11 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
   }
   if constexpr (HASRED) {
     // one partial (16 complex) per block and reduction op: slot k at partials + k*slot_stride
-    for (uint32_t i = t; i < fg.ngrad * FACC; i += BLOCK) {
+    for (uint32_t i = t; i < fg.ngrad * FACC; i += NT) {
       const uint32_t k = i / FACC, e = i % FACC;
       real s = 0;
 #pragma unroll
-      for (int w = 0; w < BLOCK / 64; ++w) s += accw[w][k][e];
+      for (int w = 0; w < NT / 64; ++w) s += accw[w][k][e];
       reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] = s;
     }
   }

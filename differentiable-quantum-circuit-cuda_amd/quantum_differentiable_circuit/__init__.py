@@ -284,6 +284,53 @@ def plan(qubits_number, world, instructions, mode, start_phys=None, precision=No
     return ops, list(end)
 
 
+def fusion_schedule(qubits_number, instructions, mode, fwd_sens=None, precision=None,
+                    lcmin=0, max_ops=0):
+    """The fused-pass scheduler of the native runtime (qdc_fusion_schedule, host only) on the
+    unsharded plan of `instructions` = [(kind, pos2[, pos1])]; mode 0 run, 1 forward,
+    2 backward.  Returns (plan, items): plan = the dicts of `plan()`, items = execution-ordered
+    [{"type": 0 single | 1 remap | 2 fused, "lc", "h", "hb", "stages": [[plan index, ...]]}]."""
+    lib = load(precision or default_precision())
+    m = len(instructions)
+    kinds_l = [int(i[0]) for i in instructions]
+    kinds = (C.c_int * m)(*kinds_l)
+    a = (C.c_uint * m)(*[int(i[1]) for i in instructions])
+    b = (C.c_uint * m)(*[int(i[2]) if len(i) > 2 else 0 for i in instructions])
+    cap = 4 * m + 16
+    raw = (PlanOp * cap)()
+    k = int(lib.qdc_plan(qubits_number, 1, kinds, a, b, m, mode, None, raw, cap, None))
+    ops = [{"type": "op", "instr": raw[i].instr, "pos2": raw[i].pos2, "pos1": raw[i].pos1}
+           for i in range(k)]
+    first_inject = 2**64 - 1
+    if mode == 2:
+        for i, o in enumerate(ops):
+            if kinds_l[o["instr"]] in (12, 13):  # DiffQ2Density, DiffQ1Density
+                first_inject = i
+                break
+    sens = (C.c_ubyte * m)(*[1 if x else 0 for x in (fwd_sens or [0] * m)])
+    icap, scap, ocap = k + 1, k + 1, k + 1
+    info = (C.c_uint * (12 * icap))()
+    slen = (C.c_uint * scap)()
+    order = (C.c_uint * ocap)()
+    n_items = int(lib.qdc_fusion_schedule(qubits_number, 1 if mode == 2 else 0, first_inject,
+                                          kinds, sens, m, raw, k, lcmin, max_ops, info, icap,
+                                          slen, scap, order, ocap))
+    if n_items == 2**64 - 1:
+        raise RuntimeError("fusion schedule output capacity exceeded")
+    items, si, oi = [], 0, 0
+    for i in range(n_items):
+        t, nst, lc, h = info[12 * i], info[12 * i + 1], info[12 * i + 2], info[12 * i + 3]
+        stages = []
+        for _ in range(nst):
+            stages.append([int(order[oi + j]) for j in range(slen[si])])
+            oi += slen[si]
+            si += 1
+        items.append({"type": int(t), "lc": int(lc), "h": int(h),
+                      "hb": [int(info[12 * i + 4 + j]) for j in range(min(h, 8))],
+                      "stages": stages})
+    return ops, items
+
+
 # ---------------------------------------------------------------------------------------
 # QuantizedTensor (src/quantized_tensor.rs:54-238) over the 18-function C ABI
 # ---------------------------------------------------------------------------------------

@@ -32,7 +32,7 @@ RUNTIME = (
     "qdc_circuit_backward", "qdc_circuit_get_state", "qdc_circuit_sync", "qdc_circuit_profile",
     "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
     "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
-    "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_plan",
+    "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_plan", "qdc_fusion_schedule",
 )
 
 
@@ -103,6 +103,10 @@ def _proto(lib):
         "qdc_plan": (_S, [_S, _S, C.POINTER(C.c_int), C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                           _S, C.c_int, C.POINTER(C.c_uint), C.POINTER(PlanOp), _S,
                           C.POINTER(C.c_uint)]),
+        "qdc_fusion_schedule": (_S, [_S, C.c_int, _S, C.POINTER(C.c_int), C.POINTER(C.c_ubyte),
+                                     _S, C.POINTER(PlanOp), _S, C.c_int, C.c_int,
+                                     C.POINTER(C.c_uint), _S, C.POINTER(C.c_uint), _S,
+                                     C.POINTER(C.c_uint), _S]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -159,6 +159,22 @@ size_t qdc_plan(size_t qubits_number, size_t world, const int* kinds, const unsi
                 const unsigned* pos1, size_t count, int mode, const unsigned* start_phys,
                 qdc_plan_op* out, size_t cap, unsigned* end_phys);
 
+/* ---- Fused-pass schedule ----------------------------------------------
+ * The runtime's own scheduler, exposed for tests and tools: which plan ops share an HBM pass
+ * and in which order they run.  kinds[n_instr]: instruction kinds; inexact[n_instr]
+ * (nullable = all 0): 1 marks a gate whose matrix is not unitary to working precision;
+ * plan[n_plan]: from qdc_plan; first_inject: plan index of the first cotangent injection
+ * (backward; SIZE_MAX otherwise); lcmin / max_ops: tile rows and pass size (<= 0: defaults).
+ * Outputs, per item in execution order: item_info[12*i ..] = {type (0 single op, 1 remap,
+ * 2 fused pass), stages, lc, h, hb[0..7]}; stage_len[]: ops per stage, flattened over items;
+ * op_order[]: plan indices in execution order.  Returns the number of items, or SIZE_MAX if an
+ * output capacity is too small. */
+size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t first_inject,
+                           const int* kinds, const unsigned char* inexact, size_t n_instr,
+                           const qdc_plan_op* plan, size_t n_plan, int lcmin, int max_ops,
+                           unsigned* item_info, size_t item_cap, unsigned* stage_len,
+                           size_t stage_cap, unsigned* op_order, size_t op_cap);
+
 #ifdef __cplusplus
 }
 #endif

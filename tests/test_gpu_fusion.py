@@ -161,8 +161,9 @@ def test_bench_circuit_batches_densities_and_injections():
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 def test_fused_densities_with_nonunitary_matrices_on_unitary_kinds(prec):
     """The reference applies whatever matrix a unitary-kind gate carries (the FD test perturbs
-    them); a density may only pass gates that are unitary to working precision, so fused
-    forward densities must still match the oracle exactly."""
+    them) and uncomputes it with U^+: a density may only pass gates unitary to working
+    precision, and in the reverse sweep such inexact gates keep their order relative to
+    variable gates, so fused densities and gradients still match the oracle."""
     dt = DT[prec]
     n = 14
     ins, const, var = O.random_circuit(n, 100, seed=77, density_every=2)
@@ -177,3 +178,7 @@ def test_fused_densities_with_nonunitary_matrices_on_unitary_kinds(prec):
     want = o.forward(cg, vg)
     c = build(prec, n, ins, 1)
     assert normrel(c.forward(cg, vg), want) < TOL[prec] / 10
+    # reverse sweep: inexact gates keep their order relative to variable gates
+    _, cots = O.tsallis_loss_and_cotangents([d.astype(np.complex128) for d in want])
+    cots = [np.ascontiguousarray(x.conj(), dtype=dt) for x in cots]
+    assert normrel(c.backward(cots, cg, vg), o.backward(cots, cg, vg)) < TOL[prec]
