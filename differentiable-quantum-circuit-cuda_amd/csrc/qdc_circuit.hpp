@@ -149,7 +149,6 @@ struct Circuit {
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
-  int fused_nt1 = 256, fused_nt2 = 256;  // threads per block of one- / two-state passes
   uint32_t last_fused_grid = 0;
   unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
   unsigned char* prog_host = nullptr;  // pinned staging
@@ -175,8 +174,6 @@ struct Circuit {
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
       fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
     if (const char* e = getenv("QDC_FUSE_MEAS")) fuse_meas = atoi(e);
-    if (const char* e = getenv("QDC_FUSED_NT1")) fused_nt1 = atoi(e) == 128 ? 128 : 256;
-    if (const char* e = getenv("QDC_FUSED_NT2")) fused_nt2 = atoi(e) == 128 ? 128 : 256;
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
@@ -627,11 +624,11 @@ struct Circuit {
   template <bool TWO, bool HASRED, bool WF>
   const char* launch_fused(const char* name, double bytes, const fgeo& fg, chunk* f, chunk* b,
                            const fop* fops, const cx* mats, cx* partials, uint64_t stride) {
-    const int nt = TWO ? fused_nt2 : fused_nt1;
+    // 256 threads per tile (measured: 128 threads with twice the quartets per thread and
+    // occupancy 2 was 2-4 % slower)
+    constexpr int NT = 256;
     uint32_t grid = 0;
-    QDC_TRY(fused_grid(fg, nt == 128 ? (const void*)fused_kernel<TWO, HASRED, WF, 128>()
-                                     : (const void*)fused_kernel<TWO, HASRED, WF, 256>(),
-                       nt, grid));
+    QDC_TRY(fused_grid(fg, (const void*)fused_kernel<TWO, HASRED, WF, NT>(), NT, grid));
     fgeo g = fg;
     uint64_t tpb = 1;
     while (tpb * grid < g.ntiles) tpb <<= 1;
@@ -639,11 +636,8 @@ struct Circuit {
     grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
-    if (nt == 128)
-      return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, 128>(), grid, 128u, f, b,
-                              fops, mats, g, partials, stride);
-    return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, 256>(), grid, 256u, f, b,
-                            fops, mats, g, partials, stride);
+    return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, NT>(), grid, (uint32_t)NT,
+                            f, b, fops, mats, g, partials, stride);
   }
   // one wave of resident blocks (occupancy query, cached per kernel), or QDC_FUSED_BLOCKS
   const char* fused_grid(const fgeo& fg, const void* kernel, int nt, uint32_t& grid) {
