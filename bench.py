@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--seed", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--local-shards", type=int, default=None,
+                    help="rehearse the sharded data path on one GPU (G shards, device copies in "
+                         "place of the RCCL all-to-all); not a multi-GPU measurement")
     ap.add_argument("--no-gate-sample", action="store_true",
                     help="skip the single-gate (fusion off) kernel sample")
     ap.add_argument("--cpu-gates", type=int, default=12,
@@ -56,10 +59,10 @@ def parse():
     return ap.parse_args()
 
 
-def build_circuit(q, n, layers, seed, precision, comm=None):
-    from oracle import oracle as O  # workload generator only (gate matrices, instruction list)
-    ins, var = O.layered_circuit(n, layers, seed)
-    c = q.circuit_class(precision)(n, comm=comm)
+def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None):
+    from quantum_differentiable_circuit import workloads as W  # synthetic C2 workload
+    ins, var = W.layered_circuit(n, layers, seed)
+    c = q.circuit_class(precision)(n, comm=comm, local_shards=local_shards)
     for kind, pos in ins:
         c._push(kind, *pos)
     dt = c.dtype
@@ -239,8 +242,8 @@ def micro(args):
 
 
 def O_haar(rng, k):
-    from oracle import oracle as O
-    return O.haar_unitary(rng, k)
+    from quantum_differentiable_circuit import workloads as W
+    return W.haar_unitary(rng, k)
 
 
 def main():
@@ -257,14 +260,16 @@ def main():
     if world > 1:
         from quantum_differentiable_circuit.distributed import Communicator
         comm = Communicator(args.precision, device=local)
-    c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision, comm)
+    c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision, comm,
+                               args.local_shards)
     ngates = len(vg)
     cots = sigma_z_cotangents(sum(1 for k, _ in ins if k in (12, 13)), c.dtype)
     remaps = 0
-    if world > 1:
+    shards = world if world > 1 else (args.local_shards or 1)
+    if shards > 1:
         instr = [(k, *p) for k, p in ins]
-        f_ops, end = q.plan(n, world, instr, 1, precision=args.precision)
-        b_ops, _ = q.plan(n, world, instr, 2, start_phys=end, precision=args.precision)
+        f_ops, end = q.plan(n, shards, instr, 1, precision=args.precision)
+        b_ops, _ = q.plan(n, shards, instr, 2, start_phys=end, precision=args.precision)
         remaps = sum(o["type"] == "remap" for o in f_ops + b_ops)
 
     for _ in range(args.warmup):
@@ -349,7 +354,9 @@ def main():
                        "qubits": n, "layers": args.layers, "gates_per_step": ngates,
                        "densities_per_step": len(cots), "state_GiB": state_gib,
                        "parallelism": (f"state sharded over {world} GPUs by high qubits, "
-                                       f"RCCL all-to-all remaps") if world > 1 else "single GPU",
+                                       f"RCCL all-to-all remaps") if world > 1 else
+                                      (f"rehearsal: {shards} shards on one GPU (device copies)"
+                                       if shards > 1 else "single GPU"),
                        "remaps_per_step": remaps},
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

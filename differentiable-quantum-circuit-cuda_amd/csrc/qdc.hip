@@ -188,7 +188,7 @@ QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned
     for (uint32_t q = 0; q < n; ++q) m.logi[m.phys[q]] = q;
   }
   std::vector<qdc_plan_op> plan;
-  qdc::plan_pass(ops, index, m, plan);
+  qdc::plan_pass(ops, index, m, plan, mode == QDC_PLAN_BACKWARD);
   for (size_t i = 0; i < plan.size() && i < cap; ++i) out[i] = plan[i];
   if (end_phys)
     for (uint32_t q = 0; q < n; ++q) end_phys[q] = m.phys[q];

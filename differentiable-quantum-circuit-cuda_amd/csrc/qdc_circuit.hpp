@@ -359,7 +359,7 @@ struct Circuit {
     active_ops(ins, mode, ops, index);
     QubitMap m = layout;
     std::vector<qdc_plan_op> out;
-    plan_pass(ops, index, m, out);
+    plan_pass(ops, index, m, out, mode == QDC_PLAN_BACKWARD, &inexact);
     return out;
   }
 
@@ -756,8 +756,8 @@ struct Circuit {
         if (is_diff_density(ins[k].kind) || (mode == QDC_MODE_RUN && is_density(ins[k].kind)))
           out_idx[k] = o++;
     }
-    const std::vector<qdc_plan_op> pl = plan(mode);
     mark_inexact(cg, vg, gidx);
+    const std::vector<qdc_plan_op> pl = plan(mode);
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
@@ -839,6 +839,7 @@ struct Circuit {
         if (is_var(ins[k].kind)) var_idx[k] = v++;
     }
     bool have_bwd = false;
+    mark_inexact(cg, vg, gidx);
     const std::vector<qdc_plan_op> pl = plan(QDC_PLAN_BACKWARD);
     size_t first_inject = pl.size();
     for (size_t i = 0; i < pl.size(); ++i)
@@ -846,7 +847,6 @@ struct Circuit {
         first_inject = i;
         break;
       }
-    mark_inexact(cg, vg, gidx);
     std::vector<Item> items = fuse_items(pl, true, first_inject);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,

@@ -11,6 +11,7 @@
 
 #include "qdc/circuit.h"
 #include "qdc_kernels.hpp"
+#include "qdc_shard.hpp"
 
 namespace qdc {
 
@@ -123,41 +124,13 @@ struct FusionPlanner {
   bool is_meas(const qdc_plan_op& op) const {
     return op.type == QDC_PLAN_OP && is_density(ins[op.instr].kind);
   }
-  // Forward: a density passes a gate on other qubits only if the gate is unitary to
-  // working precision (the reduced density is invariant under U_B only if U_B^+ U_B = I), so
-  // it is checked per call on the actual matrices (`inexact`).  Reverse sweep: the reference
-  // uncomputes every non-NonU kind with U^+ (diagonal: conj), so B = U^T = conj(A) holds by
-  // construction and an injection commutes with such const gates whatever the matrix.
-  bool is_sens(const qdc_plan_op& op, bool backward) const {
-    if (op.type != QDC_PLAN_OP) return false;
-    const int k = ins[op.instr].kind;
-    if (!(is_const(k) || is_var(k))) return false;
-    if (backward) return is_nonu(k) || is_var(k);
-    return is_nonu(k) || is_inexact(op);
-  }
-  // A non-NonU gate whose matrix is not unitary to working precision: the reference applies
-  // it as given and uncomputes it with U^+ (!= U^-1).  In the reverse sweep, swapping two gates
-  // on disjoint qubits leaves the other gate's gradient unchanged only if B^T A = I for the
-  // moved gate (A = U^-1): so an inexact gate keeps its order relative to variable gates.
-  bool is_inexact(const qdc_plan_op& op) const {
-    if (op.type != QDC_PLAN_OP || op.instr >= inexact.size()) return false;
-    const int k = ins[op.instr].kind;
-    return (is_const(k) || is_var(k)) && !is_nonu(k) && inexact[op.instr];
-  }
-  // Order classes: an op may not pass a skipped op of a conflicting class.
-  enum : uint32_t { C_MEAS = 1, C_SENS = 2, C_VAR = 4, C_INEX = 8 };
+  // order classes (qdc_shard.hpp): an op may not pass a skipped op of a conflicting class
   uint32_t op_class(const qdc_plan_op& op, bool backward) const {
-    uint32_t c = 0;
-    if (is_meas(op)) c |= C_MEAS;
-    if (is_sens(op, backward)) c |= C_SENS;
-    if (backward && op.type == QDC_PLAN_OP && is_var(ins[op.instr].kind)) c |= C_VAR;
-    if (backward && is_inexact(op)) c |= C_INEX;
-    return c;
+    if (op.type != QDC_PLAN_OP) return 0;
+    const bool inex = op.instr < inexact.size() && inexact[op.instr];
+    return order_class(ins[op.instr].kind, backward, inex);
   }
-  static uint32_t conflicts_of(uint32_t c) {
-    return ((c & C_MEAS) ? C_SENS : 0u) | ((c & C_SENS) ? C_MEAS : 0u) |
-           ((c & C_VAR) ? C_INEX : 0u) | ((c & C_INEX) ? C_VAR : 0u);
-  }
+  static uint32_t conflicts_of(uint32_t c) { return order_conflicts(c); }
   bool is_gate_op(const qdc_plan_op& op) const {
     if (op.type != QDC_PLAN_OP) return false;
     const int k = ins[op.instr].kind;

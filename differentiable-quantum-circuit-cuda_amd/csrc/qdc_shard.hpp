@@ -66,57 +66,125 @@ struct PlanIn {
   uint32_t a, b;  // logical qubits (a only for one-qubit kinds)
 };
 
-// Plan one pass over `ops` (already in execution order; `index[i]` = instruction index).
-// Emits QDC_PLAN_OP / QDC_PLAN_REMAP records; `map` is updated in place.
+// ---- order classes -------------------------------------------------------------------------
+// Ops may run out of program order (remap planning here, pass scheduling in qdc_fusion.hpp)
+// only as gates on disjoint qubits commute, with these extra constraints (an op may not pass a
+// skipped op of a conflicting class):
+//  * a density commutes with a gate on other qubits only if the gate is unitary to working
+//    precision; a cotangent injection (reverse sweep) only with const non-NonU gates, for which
+//    the pull-back B = U^T = conj(U^+) = conj(A) by construction:
+//      MEAS (densities / injections) <-> SENS (forward: NonU or inexact gates; reverse: NonU
+//      or variable gates);
+//  * reverse sweep: swapping two gates leaves the other's gradient unchanged only if the moved
+//    gate has B^T A = I, i.e. its uncompute A is the true inverse; the reference uncomputes
+//    non-NonU kinds with U^+, so a gate whose matrix is not unitary ("inexact") keeps its
+//    order relative to variable gates:  INEX <-> VAR.
+enum : uint32_t { OC_MEAS = 1, OC_SENS = 2, OC_VAR = 4, OC_INEX = 8 };
+inline bool kind_is_gate(int k) { return k >= QDC_CONST_Q2 && k <= QDC_VAR_Q1_NONU; }
+inline bool kind_is_density(int k) { return k >= QDC_Q2_DENSITY && k <= QDC_DIFF_Q1_DENSITY; }
+inline bool kind_is_var(int k) {
+  return k == QDC_VAR_Q1 || k == QDC_VAR_Q1_NONU || k == QDC_VAR_Q2 || k == QDC_VAR_Q2_NONU ||
+         k == QDC_VAR_Q2_DIAG;
+}
+inline bool kind_is_nonu(int k) {
+  return k == QDC_CONST_Q1_NONU || k == QDC_VAR_Q1_NONU || k == QDC_CONST_Q2_NONU ||
+         k == QDC_VAR_Q2_NONU;
+}
+// inexact: the gate's matrix is not unitary to working precision (per call)
+inline uint32_t order_class(int kind, bool backward, bool inexact) {
+  uint32_t c = 0;
+  if (kind_is_density(kind)) c |= OC_MEAS;
+  if (kind_is_gate(kind)) {
+    const bool inex = inexact && !kind_is_nonu(kind);
+    if (kind_is_nonu(kind) || (backward ? kind_is_var(kind) : inex)) c |= OC_SENS;
+    if (backward && kind_is_var(kind)) c |= OC_VAR;
+    if (backward && inex) c |= OC_INEX;
+  }
+  return c;
+}
+inline uint32_t order_conflicts(uint32_t c) {
+  return ((c & OC_MEAS) ? OC_SENS : 0u) | ((c & OC_SENS) ? OC_MEAS : 0u) |
+         ((c & OC_VAR) ? OC_INEX : 0u) | ((c & OC_INEX) ? OC_VAR : 0u);
+}
+
+// Plan one pass over `ops` (program execution order; `index[i]` = instruction index,
+// inexact[index] optional).  Commutation-aware: every op that is ready (no skipped earlier op
+// on its qubits or of a conflicting class) and has all qubits local runs, in program order;
+// only when nothing else can run does a REMAP swap the g global qubits with g local victims.
+// Victims: never physical position 0 (the in-chunk bit) nor a qubit of the first blocked op
+// (so it runs next: progress), farthest first use among the remaining ops first (Belady);
+// ties: highest position (the top local bits need no pack).  On a brickwork circuit the
+// global qubits' light cone grows a couple of qubits per layer, so a remap buys many layers
+// instead of one.  Emits QDC_PLAN_OP / QDC_PLAN_REMAP records; `map` is updated in place.
 inline void plan_pass(const std::vector<PlanIn>& ops, const std::vector<int>& index,
-                      QubitMap& map, std::vector<qdc_plan_op>& out) {
+                      QubitMap& map, std::vector<qdc_plan_op>& out, bool backward = false,
+                      const std::vector<uint8_t>* inexact = nullptr) {
   const uint32_t g = map.g;
-  const size_t L = ops.size();
-  // next_use[i][q] is computed lazily by a forward scan at remap time (remaps are rare)
-  auto uses = [&](size_t i, uint32_t q) {
-    return ops[i].a == q || (!instr_is_q1(ops[i].kind) && ops[i].b == q);
+  auto qmask = [&](const PlanIn& op) {
+    return (1ull << op.a) | (instr_is_q1(op.kind) ? 0ull : (1ull << op.b));
   };
-  for (size_t i = 0; i < L; ++i) {
+  auto emit = [&](size_t i) {
     const PlanIn& op = ops[i];
-    const bool q1 = instr_is_q1(op.kind);
-    const bool need = g > 0 && (!map.local(op.a) || (!q1 && !map.local(op.b)));
-    if (need) {
-      // candidates: local physical positions >= 1 (never the in-chunk bit 0), not holding an
-      // operand of this op; score = distance to the next use of the qubit they hold
-      std::vector<std::pair<size_t, uint32_t>> cand;
-      for (uint32_t p = 1; p < map.nl(); ++p) {
-        const uint32_t q = map.logi[p];
-        if (q == op.a || (!q1 && q == op.b)) continue;
-        size_t nxt = std::numeric_limits<size_t>::max();
-        for (size_t k = i + 1; k < L; ++k)
-          if (uses(k, q)) {
-            nxt = k;
-            break;
-          }
-        cand.push_back({nxt, p});
-      }
-      // farthest next use first; ties: highest position (keeps the pack coalesced, and the top
-      // local bits need no pack at all)
-      std::sort(cand.begin(), cand.end(), [](auto& x, auto& y) {
-        return x.first != y.first ? x.first > y.first : x.second > y.second;
-      });
-      qdc_plan_op r{};
-      r.type = QDC_PLAN_REMAP;
-      r.instr = -1;
-      r.nvictims = g;
-      for (uint32_t j = 0; j < g; ++j) r.victims[j] = cand[j].second;
-      std::sort(r.victims, r.victims + g);
-      r.pack = 0;
-      for (uint32_t j = 0; j < g; ++j) r.pack |= (r.victims[j] != map.nl() - g + j);
-      map.apply(r.victims);
-      out.push_back(r);
-    }
     qdc_plan_op o{};
     o.type = QDC_PLAN_OP;
     o.instr = index[i];
     o.pos2 = map.phys[op.a];
-    o.pos1 = q1 ? o.pos2 : map.phys[op.b];
+    o.pos1 = instr_is_q1(op.kind) ? o.pos2 : map.phys[op.b];
     out.push_back(o);
+  };
+  std::vector<uint32_t> cls(ops.size());
+  for (size_t i = 0; i < ops.size(); ++i) {
+    const bool inex = inexact && (size_t)index[i] < inexact->size() && (*inexact)[index[i]];
+    cls[i] = order_class(ops[i].kind, backward, inex);
+  }
+  std::vector<size_t> rem(ops.size());
+  for (size_t i = 0; i < ops.size(); ++i) rem[i] = i;
+  while (!rem.empty()) {
+    uint64_t blocked = 0;
+    uint32_t left = 0;
+    std::vector<size_t> rest;
+    for (size_t i : rem) {
+      const PlanIn& op = ops[i];
+      const uint64_t q = qmask(op);
+      const bool local = map.local(op.a) && (instr_is_q1(op.kind) || map.local(op.b));
+      if ((q & blocked) || (order_conflicts(cls[i]) & left) || !local) {
+        blocked |= q;
+        left |= cls[i];
+        rest.push_back(i);
+        continue;
+      }
+      emit(i);
+    }
+    rem.swap(rest);
+    if (rem.empty()) break;
+    // remap: the first remaining op is blocked only by a global qubit
+    const PlanIn& first = ops[rem[0]];
+    const uint64_t keep = qmask(first);
+    std::vector<std::pair<size_t, uint32_t>> cand;
+    for (uint32_t p = 1; p < map.nl(); ++p) {
+      const uint32_t q = map.logi[p];
+      if (keep >> q & 1ull) continue;
+      size_t nxt = std::numeric_limits<size_t>::max();
+      for (size_t k = 0; k < rem.size(); ++k)
+        if (qmask(ops[rem[k]]) >> q & 1ull) {
+          nxt = k;
+          break;
+        }
+      cand.push_back({nxt, p});
+    }
+    std::sort(cand.begin(), cand.end(), [](auto& x, auto& y) {
+      return x.first != y.first ? x.first > y.first : x.second > y.second;
+    });
+    qdc_plan_op r{};
+    r.type = QDC_PLAN_REMAP;
+    r.instr = -1;
+    r.nvictims = g;
+    for (uint32_t j = 0; j < g; ++j) r.victims[j] = cand[j].second;
+    std::sort(r.victims, r.victims + g);
+    r.pack = 0;
+    for (uint32_t j = 0; j < g; ++j) r.pack |= (r.victims[j] != map.nl() - g + j);
+    map.apply(r.victims);
+    out.push_back(r);
   }
 }
 

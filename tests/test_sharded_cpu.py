@@ -83,7 +83,9 @@ def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
             gidx[i], ci = const[ci], ci + 1
         elif k not in (O.Q1_DENSITY, O.Q2_DENSITY, O.DIFF_Q1_DENSITY, O.DIFF_Q2_DENSITY):
             gidx[i], vi = var[vi], vi + 1
-    dens = []
+    # the planner may run ops out of program order (commuting ones): densities and
+    # cotangents are keyed by instruction, as in the runtime
+    dens = {}
     nremap = 0
     for op in ops:
         if op["type"] == "remap":
@@ -92,18 +94,18 @@ def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
             continue
         k = kinds[op["instr"]]
         if k == O.DIFF_Q1_DENSITY:
-            dens.append(O.get_q1_density(shard, op["pos2"]))
+            dens[op["instr"]] = O.get_q1_density(shard, op["pos2"])
         elif k == O.DIFF_Q2_DENSITY:
-            dens.append(O.get_q2_density(shard, op["pos2"], op["pos1"]))
+            dens[op["instr"]] = O.get_q2_density(shard, op["pos2"], op["pos1"])
         else:
             shard = apply(shard, k, op["pos2"], op["pos1"], gidx[op["instr"]])
-    dens = [allreduce(d).reshape(int(np.sqrt(d.size)), -1) for d in dens]
-    cots = cot_fn(dens)
+    order = sorted(dens)
+    dens = [allreduce(dens[i]).reshape(int(np.sqrt(dens[i].size)), -1) for i in order]
+    cot_of = dict(zip(order, cot_fn(dens)))
     # backward (Circuit::backward): reverse order, starting from the forward's final layout
     ops, _ = q.plan(n, world, instr, mode=2, start_phys=phys_end, precision="f64")
     bwd = None
     grads = {}
-    di = len(cots)
     for op in ops:
         if op["type"] == "remap":
             shard = remap(shard, op, nl, world)
@@ -115,9 +117,8 @@ def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
         k = kinds[i]
         p2, p1 = op["pos2"], op["pos1"]
         if k in (O.DIFF_Q1_DENSITY, O.DIFF_Q2_DENSITY):
-            di -= 1
             add = 2 * shard.conj()
-            gt = O.transpose(cots[di])
+            gt = O.transpose(cot_of[i])
             add = O.apply_q1_gate(add, gt, p2) if k == O.DIFF_Q1_DENSITY else O.apply_q2_gate(add, gt, p2, p1)
             bwd = add if bwd is None else bwd + add
             continue
