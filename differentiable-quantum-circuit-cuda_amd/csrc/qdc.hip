@@ -284,3 +284,25 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   }
   return items.size();
 }
+
+QDC_API size_t qdc_rq_plan(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+                           const unsigned* t2, const unsigned long long* deps, size_t n,
+                           unsigned* steps, size_t cap) {
+  std::vector<qdc::RqStage> st(n);
+  for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits);
+  if (plan.steps.size() + 2 > cap) return SIZE_MAX;
+  auto put = [&](size_t i, unsigned kind, unsigned stage, unsigned cs, const qdc::RqLayout& L) {
+    unsigned* o = steps + 7 * i;
+    o[0] = kind;
+    o[1] = stage;
+    o[2] = cs;
+    for (int s = 0; s < 4; ++s) o[3 + s] = L.slot[s];
+  };
+  put(0, 2u, 0u, 0u, plan.load);
+  for (size_t i = 0; i < plan.steps.size(); ++i)
+    put(i + 1, plan.steps[i].relayout ? 1u : 0u, plan.steps[i].stage, plan.steps[i].cs,
+        plan.steps[i].L);
+  put(plan.steps.size() + 1, 3u, 0u, 0u, plan.store);
+  return plan.steps.size() + 2;
+}

@@ -146,6 +146,8 @@ struct Circuit {
   uint32_t fuse_max_ops = FMAX_OPS;
   uint32_t fuse_lcmin = 3;  // min contiguous chunk bits of a fused tile (128-B rows)
   int fuse_meas = 1;        // densities / cotangent injections join fused passes
+  int use_rq = 1;           // f32 gate passes run register-resident (qdc_rq.hpp)
+  int rq_stats = 0;
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
@@ -174,6 +176,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
       fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
     if (const char* e = getenv("QDC_FUSE_MEAS")) fuse_meas = atoi(e);
+    if (const char* e = getenv("QDC_RQ")) use_rq = atoi(e);
+    if (const char* e = getenv("QDC_RQ_STATS")) rq_stats = atoi(e);
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
@@ -370,6 +374,9 @@ struct Circuit {
     bool has_red = false;      // reduction ops (Gamma stages or densities)
     bool writes_f = false;     // gate stages (fwd changes; else fwd is only read)
     std::vector<uint32_t> grad_slots;  // reduction slot of each reduction op, in op order
+    bool rq = false;   // register-resident pass (qdc_rq.hpp): k_rq, ops include relayouts
+    uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
+    uint32_t tbits = 0;  // amplitude bits of the tile
   };
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
   static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
@@ -447,8 +454,11 @@ struct Circuit {
         nops += stages_of[ii].size();
       }
     if (nops == 0) return nullptr;
-    mats_off = ((nops * sizeof(fop) + 255) / 256) * 256;
-    const size_t bytes = mats_off + nops * 32 * sizeof(cx);  // <= 2 R^2 = 32 per op
+    // register-resident passes add relayout ops (<= one per stage, plus the return to L0) and
+    // 12-cx layout descriptors (one per relayout, plus L0)
+    const size_t nfops = 2 * nops + items.size();
+    mats_off = ((nfops * sizeof(fop) + 255) / 256) * 256;
+    const size_t bytes = mats_off + (nops * 32 + nfops * 12 + items.size() * 32) * sizeof(cx);  // <= 2 R^2 = 32 per stage
     if (bytes > prog_cap) {
       QDC_HIP(hipStreamSynchronize(ctx.stream));
       if (prog_dev) QDC_HIP(hipFree(prog_dev));
@@ -471,6 +481,22 @@ struct Circuit {
       const bool two = backward && it.ops[0] >= first_inject;
       it.has_red = false;
       it.writes_f = false;
+      std::vector<fop> pf;  // the pass's stage ops in program order
+      std::vector<uint64_t> pq;  // their qubits (physical positions)
+      std::vector<uint32_t> pc;  // their order classes (qdc_fusion.hpp)
+      std::vector<int> pslot;    // their reduction slot (Gamma stages), else -1
+      pf.reserve(stages_of[ii].size());
+      const FusionPlanner PL = planner();
+      for (const auto& st : stages_of[ii]) {
+        uint64_t q = 0;
+        uint32_t c = 0;
+        for (uint32_t pi : st) {
+          q |= (1ull << plan[pi].pos2) | (1ull << plan[pi].pos1);
+          c |= PL.op_class(plan[pi], backward);
+        }
+        pq.push_back(q);
+        pc.push_back(c);
+      }
       auto local_bit = [&](uint32_t p) -> uint32_t {
         if (p < (uint32_t)LV + it.lc) return p;
         for (uint32_t r = 0; r < it.h; ++r)
@@ -483,7 +509,9 @@ struct Circuit {
           const Instr& in = ins[op.instr];
           const bool q1 = is_q1_density(in.kind);
           const int R = q1 ? 2 : 4;
-          fop& F = fops[fo++];
+          pf.emplace_back();
+          pslot.push_back(-1);
+          fop& F = pf.back();
           F.t1 = local_bit(q1 ? op.pos2 : op.pos1);
           F.t2 = local_bit(op.pos2);
           F.mat = (uint32_t)mo;
@@ -581,7 +609,9 @@ struct Circuit {
           A = Anew;
           B = smat_mul(Eb, B);
         }
-        fop& F = fops[fo++];
+        pf.emplace_back();
+        pslot.push_back(-1);
+        fop& F = pf.back();
         F.t1 = local_bit(lo);
         F.t2 = local_bit(hi);
         F.mat = (uint32_t)mo;
@@ -603,11 +633,65 @@ struct Circuit {
         if (any_grad) {
           post.slot = next_slot++;
           it.grad_slots.push_back(post.slot);
+          pslot.back() = (int)post.slot;
           it.has_red = true;
           stage_post.push_back(std::move(post));
         }
       }
-      it.nstage = (uint32_t)stages_of[ii].size();
+      // register-resident pass: f32, gate stages only (no densities / injections)
+      bool rq = use_rq && sizeof(real) == 4 && it.writes_f;
+      for (const fop& F : pf) rq = rq && (F.kind & 7u) <= FK_DIAG;
+      it.rq = rq;
+      it.tbits = (uint32_t)LV + it.lc + it.h;
+      if (!rq) {
+        for (const fop& F : pf) fops[fo++] = F;
+        it.nstage = (uint32_t)pf.size();
+        continue;
+      }
+      auto put_layout = [&](const RqLayout& L) {
+        const rq_layout d = rq_descriptor(L, it.tbits);
+        const uint32_t off = (uint32_t)mo;
+        std::memcpy(&mats[mo], &d, sizeof d);
+        mo += sizeof(rq_layout) / sizeof(cx);
+        return off;
+      };
+      std::vector<RqStage> rs;
+      for (size_t k = 0; k < pf.size(); ++k) {
+        RqStage r{pf[k].kind & 7u, pf[k].t1, pf[k].t2, 0};
+        for (size_t i = 0; i < k; ++i)
+          if ((pq[i] & pq[k]) || (FusionPlanner::conflicts_of(pc[i]) & pc[k]) ||
+              (FusionPlanner::conflicts_of(pc[k]) & pc[i]))
+            r.deps |= 1ull << i;
+        rs.push_back(r);
+      }
+      const RqPlan P = rq_plan(rs, it.tbits);
+      it.l0 = put_layout(P.load);
+      {  // rqio after the load descriptor
+        rqio io{};
+        rq_hbm(P.load, it.tbits, it.lc, it.hb, io.gv_ld, io.offi_ld);
+        rq_hbm(P.store, it.tbits, it.lc, it.hb, io.gv_st, io.offi_st);
+        std::memcpy(&mats[mo], &io, sizeof io);
+        mo += sizeof(rqio) / sizeof(cx);
+      }
+      uint32_t n = 0;
+      it.grad_slots.clear();  // the kernel reduces Gamma stages in execution order
+      for (const RqStep& step : P.steps) {
+        if (!step.relayout && pslot[step.stage] >= 0)
+          it.grad_slots.push_back((uint32_t)pslot[step.stage]);
+        fop F{};
+        if (step.relayout) {
+          F.kind = FK_RELAYOUT;
+          F.mat = put_layout(step.L);
+        } else {
+          F = pf[step.stage];
+          F.t1 = step.cs;
+          F.t2 = 0;
+        }
+        fops[fo++] = F;
+        ++n;
+      }
+      it.nstage = n;
+      if (rq_stats) fprintf(stderr, "rq pass: %zu stages, %u ops (T=%u lc=%u)\n", pf.size(), n, it.tbits, it.lc);
     }
     QDC_HIP(hipMemcpyAsync(prog_dev, prog_host, mats_off + mo * sizeof(cx),
                            hipMemcpyHostToDevice, ctx.stream));
@@ -638,6 +722,41 @@ struct Circuit {
     last_fused_grid = grid;
     return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, NT>(), grid, (uint32_t)NT,
                             f, b, fops, mats, g, partials, stride);
+  }
+  // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
+  const char* launch_rq(const char* name, double bytes, const fgeo& fg, bool two, uint32_t tbits,
+                        uint32_t l0, chunk* f, chunk* b, const fop* fops, const cx* mats,
+                        cx* partials, uint64_t stride) {
+#ifndef QDC_F64
+    const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
+    const void* kern = nullptr;
+    if (two && nt == 128) kern = (const void*)k_rq<true, 128>;
+    else if (!two && nt == 128) kern = (const void*)k_rq<false, 128>;
+    else if (!two && nt == 256) kern = (const void*)k_rq<false, 256>;
+    else return fail("no register-resident kernel for a %u-amplitude %s tile", 1u << tbits,
+                     two ? "two-state" : "one-state");
+    uint32_t grid = 0;
+    QDC_TRY(fused_grid(fg, kern, (int)nt, grid));
+    fgeo g = fg;
+    uint64_t tpb = 1;
+    while (tpb * grid < g.ntiles) tpb <<= 1;
+    g.tpb = (uint32_t)tpb;
+    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
+    last_fused_grid = grid;
+    if (two)
+      return ctx.launch_block(name, bytes, k_rq<true, 128>, grid, nt, f, b, fops, mats, g, l0,
+                              partials, stride);
+    if (nt == 128)
+      return ctx.launch_block(name, bytes, k_rq<false, 128>, grid, nt, f, b, fops, mats, g, l0,
+                              partials, stride);
+    return ctx.launch_block(name, bytes, k_rq<false, 256>, grid, nt, f, b, fops, mats, g, l0,
+                            partials, stride);
+#else
+    (void)name; (void)bytes; (void)fg; (void)two; (void)tbits; (void)l0; (void)f; (void)b;
+    (void)fops; (void)mats; (void)partials; (void)stride;
+    return fail("register-resident passes are f32 only");
+#endif
   }
   // one wave of resident blocks (occupancy query, cached per kernel), or QDC_FUSED_BLOCKS
   const char* fused_grid(const fgeo& fg, const void* kernel, int nt, uint32_t& grid) {
@@ -693,7 +812,9 @@ struct Circuit {
       }
       const uint64_t stride = (uint64_t)NBMAX * RED;
       ctx.next_flops = flops;
-      if (two) {
+      if (it.rq) {
+        QDC_TRY(launch_rq(name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride));
+      } else if (two) {
         if (it.writes_f)
           QDC_TRY((launch_fused<true, true, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
         else

@@ -11,6 +11,7 @@
 
 #include "qdc/circuit.h"
 #include "qdc_kernels.hpp"
+#include "qdc_rq.hpp"
 #include "qdc_shard.hpp"
 
 namespace qdc {
@@ -261,5 +262,205 @@ struct FusionPlanner {
   }
 
 };
+
+// ---- register layouts of a register-resident pass (qdc_rq.hpp) -----------------------------
+// A stage of the pass, in tile bits: kind FK_Q1 (t1 == t2), FK_Q2 or FK_DIAG (t1 < t2); deps =
+// the earlier stages of the pass it must follow (shared qubit or conflicting order classes).
+struct RqStage {
+  uint32_t kind, t1, t2;
+  uint64_t deps = 0;
+};
+struct RqLayout {
+  uint32_t slot[4];  // tile bit held by register slot s
+  bool operator==(const RqLayout& o) const {
+    return slot[0] == o.slot[0] && slot[1] == o.slot[1] && slot[2] == o.slot[2] &&
+           slot[3] == o.slot[3];
+  }
+  int find(uint32_t q) const {
+    for (int s = 0; s < 4; ++s)
+      if (slot[s] == q) return s;
+    return -1;
+  }
+  bool holds(uint32_t q) const { return find(q) >= 0; }
+  // HBM layouts (load / store): slot 0 = tile bit 0 (a 16-B chunk is one thread's register
+  // pair) and tile bits 1..3 are thread bits 0..2 (lanes 0..7 read 128 contiguous bytes)
+  bool hbm_ok() const {
+    return slot[0] == 0 && !holds(1) && !holds(2) && !holds(3);
+  }
+};
+// One step of a planned pass: a relayout to L, or stage `stage` run with slot case `cs`
+// (qdc_rq.hpp: S1 * 4 + S2 for two-qubit / diagonal stages, the slot for one-qubit ones).
+struct RqStep {
+  bool relayout;
+  RqLayout L;
+  uint32_t stage, cs;
+};
+struct RqPlan {
+  RqLayout load, store;
+  std::vector<RqStep> steps;
+};
+
+// The layout's LDS descriptor (qdc_rq.hpp rq_layout): rp[j] = swz(dep(j -> slots)),
+// tv[k] = swz(1 << k-th thread bit), thread bits = tile bits not in a slot, ascending.
+inline rq_layout rq_descriptor(const RqLayout& L, uint32_t T) {
+  rq_layout d{};
+  for (uint32_t j = 0; j < (uint32_t)RQ_R; ++j) {
+    uint32_t idx = 0;
+    for (int s = 0; s < 4; ++s)
+      if ((j >> s) & 1u) idx |= 1u << L.slot[s];
+    d.rp[j] = swz(idx);
+  }
+  uint32_t k = 0;
+  for (uint32_t q = 0; q < T && k < 8; ++q)
+    if (!L.holds(q)) d.tv[k++] = swz(1u << q);
+  return d;
+}
+// The HBM side of a load / store layout (rqio halves): chunk offsets of the thread bits and of
+// the register chunk index (slots 1..3), with tile chunk bit c at global chunk bit
+// c (c < lc) or hb[c - lc].
+inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* hb,
+                   uint64_t* gv, uint64_t* offi) {
+  auto gbit = [&](uint32_t tile_bit) -> uint64_t {  // tile bit >= 1 -> global chunk offset
+    const uint32_t c = tile_bit - 1;
+    return 1ull << (c < lc ? c : hb[c - lc]);
+  };
+  uint32_t k = 0;
+  for (uint32_t q = 0; q < T && k < 8; ++q)
+    if (!L.holds(q)) gv[k++] = gbit(q);
+  for (; k < 8; ++k) gv[k] = 0;
+  for (uint32_t i = 0; i < (uint32_t)RQ_R / 2; ++i) {
+    uint64_t o = 0;
+    for (int s = 1; s < 4; ++s)
+      if ((i >> (s - 1)) & 1u) o += gbit(L.slot[s]);
+    offi[i] = o;
+  }
+}
+
+// Schedule a pass's stages on register layouts (T tile bits).  List scheduling: among the
+// stages whose dependencies are done, run (lowest index first) one whose qubits sit in
+// register slots; when none does, relayout to the 4 qubits of the lowest ready stage plus
+// those of the stages that then become runnable, greedily in index order (a cover of the
+// coming stages), filled with the qubits of the next stages.  The pass starts in a load
+// layout chosen the same way under the HBM constraint, and ends in an HBM-valid layout.
+inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T) {
+  const size_t n = st.size();
+  auto qset = [&](size_t j, uint32_t* q) -> int {
+    q[0] = st[j].t1;
+    q[1] = st[j].t2;
+    return st[j].t1 == st[j].t2 ? 1 : 2;
+  };
+  auto fits = [&](const RqLayout& L, size_t j) {
+    return L.holds(st[j].t1) && L.holds(st[j].t2);
+  };
+  auto hbm_allowed = [](uint32_t q) { return q == 0 || q > 3; };
+  // the qubit set of a relayout: stage j0 first, then greedily the stages that become ready
+  auto cover = [&](uint64_t done, size_t j0, std::vector<uint32_t> S, bool hbm) {
+    auto add = [&](size_t j) {
+      uint32_t q[2];
+      const int m = qset(j, q);
+      std::vector<uint32_t> T2 = S;
+      for (int i = 0; i < m; ++i) {
+        if (hbm && !hbm_allowed(q[i])) return false;
+        if (std::find(T2.begin(), T2.end(), q[i]) == T2.end()) T2.push_back(q[i]);
+      }
+      if (T2.size() > 4) return false;
+      S = T2;
+      return true;
+    };
+    uint64_t sim = done;
+    if (j0 < n && add(j0)) sim |= 1ull << j0;
+    for (bool progress = true; progress;) {
+      progress = false;
+      for (size_t c = 0; c < n && !progress; ++c) {
+        if ((sim >> c) & 1ull) continue;
+        if ((st[c].deps & ~sim) != 0) continue;
+        if (add(c)) {
+          sim |= 1ull << c;
+          progress = true;
+        }
+      }
+    }
+    // fill: qubits of the next stages in index order, then the lowest allowed bits
+    for (size_t c = 0; c < n && S.size() < 4; ++c) {
+      if ((sim >> c) & 1ull) continue;
+      uint32_t q[2];
+      const int m = qset(c, q);
+      for (int i = 0; i < m && S.size() < 4; ++i)
+        if ((!hbm || hbm_allowed(q[i])) && std::find(S.begin(), S.end(), q[i]) == S.end())
+          S.push_back(q[i]);
+    }
+    for (uint32_t q = T; q-- > 0 && S.size() < 4;)
+      if ((!hbm || hbm_allowed(q)) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
+    return S;
+  };
+  // slots for a qubit set: members of `prev` keep their slot, slot 0 = bit 0 if `hbm`
+  auto place = [&](const std::vector<uint32_t>& S, const RqLayout& prev, bool hbm) {
+    RqLayout L{{~0u, ~0u, ~0u, ~0u}};
+    if (hbm) L.slot[0] = 0;
+    for (uint32_t q : S) {
+      if (L.holds(q)) continue;
+      const int ps = prev.find(q);
+      if (ps >= 0 && L.slot[ps] == ~0u) L.slot[ps] = q;
+    }
+    for (uint32_t q : S) {
+      if (L.holds(q)) continue;
+      for (int s = 0; s < 4; ++s)
+        if (L.slot[s] == ~0u) {
+          L.slot[s] = q;
+          break;
+        }
+    }
+    return L;
+  };
+  RqPlan P;
+  uint64_t done = 0;
+  {  // load layout
+    size_t j0 = n;
+    for (size_t j = 0; j < n && j0 == n; ++j) {
+      uint32_t q[2];
+      const int m = qset(j, q);
+      bool ok = st[j].deps == 0;
+      for (int i = 0; i < m; ++i) ok = ok && hbm_allowed(q[i]);
+      if (ok) j0 = j;
+    }
+    const RqLayout none{{~0u, ~0u, ~0u, ~0u}};
+    P.load = place(cover(0, j0, {0u}, true), none, true);
+  }
+  RqLayout cur = P.load;
+  for (size_t left = n; left > 0;) {
+    size_t pick = n, first_ready = n;
+    for (size_t j = 0; j < n; ++j) {
+      if (((done >> j) & 1ull) || (st[j].deps & ~done) != 0) continue;
+      if (first_ready == n) first_ready = j;
+      if (fits(cur, j)) {
+        pick = j;
+        break;
+      }
+    }
+    if (pick == n) {
+      cur = place(cover(done, first_ready, {}, false), cur, false);
+      P.steps.push_back(RqStep{true, cur, 0, 0});
+      pick = first_ready;
+    }
+    const RqStage& s = st[pick];
+    const uint32_t cs = s.kind == FK_Q1 ? (uint32_t)cur.find(s.t1)
+                                        : (uint32_t)(cur.find(s.t1) * 4 + cur.find(s.t2));
+    P.steps.push_back(RqStep{false, cur, (uint32_t)pick, cs});
+    done |= 1ull << pick;
+    --left;
+  }
+  if (cur.hbm_ok()) {
+    P.store = cur;
+  } else {
+    std::vector<uint32_t> S{0u};
+    for (int s = 0; s < 4; ++s)
+      if (hbm_allowed(cur.slot[s]) && cur.slot[s] != 0) S.push_back(cur.slot[s]);
+    for (uint32_t q = T; q-- > 0 && S.size() < 4;)
+      if (hbm_allowed(q) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
+    P.store = place(S, cur, true);
+    P.steps.push_back(RqStep{true, P.store, 0, 0});
+  }
+  return P;
+}
 
 }  // namespace qdc

@@ -1,0 +1,378 @@
+// qdc_rq.hpp — register-resident fused passes (f32): the tile lives in VGPRs, LDS is only the
+// exchange network between register layouts.
+//
+// k_fused (qdc_kernels.hpp) keeps a pass's tile in LDS and makes one LDS round trip, one
+// barrier, one accumulator init and one 64-lane Gamma reduction per stage for the two quartets
+// each thread owns.  At C2 n=28 that overhead is ~45 % of the reverse kernel's VALU stream, and
+// the tile cannot grow: LDS (160 KiB/CU) is what bounds occupancy.  Here each thread holds
+// R = 16 amplitudes of every state in registers (the VGPR file is 512 KiB/CU): 4 "register
+// qubits" (slots 0..3) and log2(NT) "thread qubits".  A stage whose qubits sit in register
+// slots runs on registers only, over 4 quartets per thread (8 one-qubit pairs): no LDS, no
+// barrier, twice the quartets per Gamma reduction.  When the next stage needs other qubits in
+// registers, a RELAYOUT op writes the state to LDS in the current layout and reads it back in
+// the new one (one state at a time through one buffer, so a block needs 2^T * 8 B of LDS).
+// The host (qdc_fusion.hpp, rq_plan) chooses the layouts: slots form two pairs {0,1}, {2,3};
+// a two-qubit stage occupies one pair (either orientation), a one-qubit stage any slot, and
+// the slot pair (or slot) to replace is the one whose qubits are needed again last.
+//
+// Layout L: tile bits of slots 0..3 plus the remaining tile bits as thread bits (ascending).
+// Amplitude (thread t, register j) sits at tile index dep(t -> thread bits) | dep(j -> slots).
+// LDS index = swz(...) = swz(dep(t)) ^ swz(dep(j)): a per-thread part tp (from the layout's
+// swizzled thread-bit vectors tv[]) XOR a uniform part rp[j].  L0 (load/store layout): slot 0 =
+// tile bit 0 (the two amplitudes of a 16-B chunk), slots 1..3 = the top three tile bits, thread
+// bits = tile bits 1..T-4 — so register pair (2i, 2i+1) is chunk t + i*NT, as in k_fused, and
+// loads/stores go straight between HBM and registers.  Every program ends in L0.
+#pragma once
+
+#include "qdc_kernels.hpp"
+
+namespace qdc {
+
+constexpr int RQ_R = 16;  // amplitudes per thread per state
+constexpr uint32_t FK_RELAYOUT = 7;
+constexpr int RQ_NT_ONE = 256;  // threads per one-state tile: 2^12 amplitudes = TILE_CHUNKS_1
+constexpr int RQ_NT_TWO = 128;  // threads per two-state tile: 2^11 amplitudes = TILE_CHUNKS_2
+
+// a register layout in the program's matrix area (12 cx = 96 B)
+struct rq_layout {
+  uint32_t rp[RQ_R];  // swz(dep(j -> slots)), in cx units
+  uint32_t tv[8];     // swz(1 << thread bit k), in cx units (k < log2 NT)
+};
+static_assert(sizeof(rq_layout) == 96, "rq_layout is 12 complex of the program");
+
+// HBM addressing of a tile's registers (after the load layout's descriptor in the program).
+// Register pair (2i, 2i+1) of thread t is one 16-B chunk (slot 0 = tile bit 0); its chunk
+// offset from the tile base is thr(t) + offi[i], thr(t) = sum of gv[k] over the set bits k of
+// t (thread bit k's chunk offset) and offi[i] = the offset of register chunk bits i (slots 1..3).
+// The load layout (the pass's first) and the store layout (its last) may differ.
+struct rqio {
+  uint64_t gv_ld[8], offi_ld[RQ_R / 2], gv_st[8], offi_st[RQ_R / 2];
+};
+static_assert(sizeof(rqio) == 256, "rqio is 32 complex of the program");
+
+#ifndef QDC_F64
+
+// fop.t1 of a register stage = slot case: two-qubit / diagonal: 2P + O for slot pair P with
+// t1 (the stage's low qubit) in slot 2P + O and t2 in the other slot of the pair; one-qubit: slot.
+template <int S1, int S2>
+__device__ __forceinline__ constexpr int rq_el(int base, int r) {
+  return base | ((r & 1) << S1) | ((r >> 1) << S2);
+}
+template <int S1, int S2>
+__device__ __forceinline__ constexpr int rq_base(int k) {  // k-th index with bits S1, S2 zero
+  int b = 0, bit = 0;
+  for (int s = 0; s < 4; ++s) {
+    if (s == S1 || s == S2) continue;
+    if ((k >> bit) & 1) b |= 1 << s;
+    ++bit;
+  }
+  return b;
+}
+
+// two-qubit stage on registers: f <- A f [, Gamma += b0 f0^T, b <- B b]
+template <int S1, int S2, bool TWO>
+__device__ __forceinline__ void rq_q2(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+                                      bool gamma, real* acc_out) {
+  cx A[16], B[16];
+  if (TWO && gamma) {
+    cx acc[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int base = rq_base<S1, S2>(k);
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const cx bp = b[rq_el<S1, S2>(base, p)], fq = f[rq_el<S1, S2>(base, q)];
+          acc[p * 4 + q] = k == 0 ? vcmul(bp, fq) : vcfma(bp, fq, acc[p * 4 + q]);
+        }
+    }
+    real v[32];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      v[2 * i] = acc[i].x;
+      v[2 * i + 1] = acc[i].y;
+    }
+    wave_reduce_add<32>(v, acc_out);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) A[i] = M[i];
+  // f with A, then b with B: one matrix (32 SGPRs) live at a time
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int base = rq_base<S1, S2>(k);
+    cx x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = f[rq_el<S1, S2>(base, r)];
+    umatvec<4>(A, x);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[rq_el<S1, S2>(base, r)] = x[r];
+  }
+  if constexpr (TWO) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int base = rq_base<S1, S2>(k);
+      cx x[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = b[rq_el<S1, S2>(base, r)];
+      umatvec<4>(B, x);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b[rq_el<S1, S2>(base, r)] = x[r];
+    }
+  }
+}
+
+// diagonal two-qubit stage: element r = 2 bit(t2) + bit(t1) of each quartet takes entry r
+template <int S1, int S2, bool TWO>
+__device__ __forceinline__ void rq_diag(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+                                        bool gamma, real* acc_out) {
+  cx A[4], B[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) A[i] = M[i];
+  if constexpr (TWO) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
+  }
+  if (TWO && gamma) {
+    cx acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int base = rq_base<S1, S2>(k);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = rq_el<S1, S2>(base, r);
+        acc[r] = k == 0 ? vcmul(b[e], f[e]) : vcfma(b[e], f[e], acc[r]);
+      }
+    }
+    real v[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = acc[i].x;
+      v[2 * i + 1] = acc[i].y;
+    }
+    wave_reduce_add<8>(v, acc_out);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int base = rq_base<S1, S2>(k);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = rq_el<S1, S2>(base, r);
+      f[e] = ucmul(A[r], f[e]);
+      if constexpr (TWO) b[e] = ucmul(B[r], b[e]);
+    }
+  }
+}
+
+// one-qubit stage on slot S: pairs (j, j | 1 << S)
+template <int S, bool TWO>
+__device__ __forceinline__ void rq_q1(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+                                      bool gamma, real* acc_out) {
+  cx A[4], B[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) A[i] = M[i];
+  if constexpr (TWO) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) B[i] = M[4 + i];
+  }
+  constexpr int LOWM = (1 << S) - 1;
+  if (TWO && gamma) {
+    cx acc[4];
+#pragma unroll
+    for (int k = 0; k < RQ_R / 2; ++k) {
+      const int j0 = ((k & ~LOWM) << 1) | (k & LOWM), j1 = j0 | (1 << S);
+      const cx bx[2] = {b[j0], b[j1]}, fx[2] = {f[j0], f[j1]};
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc[p * 2 + q] = k == 0 ? vcmul(bx[p], fx[q]) : vcfma(bx[p], fx[q], acc[p * 2 + q]);
+    }
+    real v[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = acc[i].x;
+      v[2 * i + 1] = acc[i].y;
+    }
+    wave_reduce_add<8>(v, acc_out);
+  }
+#pragma unroll
+  for (int k = 0; k < RQ_R / 2; ++k) {
+    const int j0 = ((k & ~LOWM) << 1) | (k & LOWM), j1 = j0 | (1 << S);
+    cx x[2] = {f[j0], f[j1]};
+    umatvec<2>(A, x);
+    f[j0] = x[0];
+    f[j1] = x[1];
+    if constexpr (TWO) {
+      cx y[2] = {b[j0], b[j1]};
+      umatvec<2>(B, y);
+      b[j0] = y[0];
+      b[j1] = y[1];
+    }
+  }
+}
+
+// per-thread part of a layout's LDS index
+template <int LOGNT>
+__device__ __forceinline__ uint32_t rq_tp(const rq_layout* L, uint32_t t) {
+  uint32_t tp = 0;
+#pragma unroll
+  for (int k = 0; k < LOGNT; ++k) tp ^= ((t >> k) & 1u) ? L->tv[k] : 0u;
+  return tp;
+}
+
+// move one state from layout (tp, Lc) to (tpn, Ln) through the LDS buffer
+__device__ __forceinline__ void rq_exchange(cx (&x)[RQ_R], cx* buf, uint32_t tp,
+                                            const rq_layout* Lc, uint32_t tpn,
+                                            const rq_layout* Ln) {
+  __syncthreads();  // every thread is done reading the buffer's previous contents
+#pragma unroll
+  for (int j = 0; j < RQ_R; ++j) buf[tp ^ Lc->rp[j]] = x[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RQ_R; ++j) x[j] = buf[tpn ^ Ln->rp[j]];
+}
+
+// TWO: fwd and bwd (reverse sweep, Gamma stages reduce into partials); else fwd only.
+// fg.nops ops at `ops`; at mats + l0 the load layout's descriptor, then rqio.
+template <bool TWO, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
+void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
+          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
+          uint64_t slot_stride) {
+  constexpr int LOGNT = NT == 64 ? 6 : NT == 128 ? 7 : NT == 256 ? 8 : 9;
+  constexpr int CPT = RQ_R / VEC;  // chunks of each state per thread (8)
+  constexpr int TA = NT * RQ_R;    // amplitudes per tile and state
+  __shared__ cx buf[TA];
+  __shared__ real accw[TWO ? NT / 64 : 1][TWO ? FMAX_GRAD : 1][FACC];
+  const uint32_t t = threadIdx.x;
+  const int wave = (int)(t >> 6);
+  if constexpr (TWO) {
+    for (uint32_t i = t; i < (NT / 64) * FMAX_GRAD * FACC; i += NT) (&accw[0][0][0])[i] = 0;
+    // a wave's accumulators are zeroed partly by other waves; a Gamma stage can come before
+    // the pass's first relayout barrier
+    __syncthreads();
+  }
+  const rq_layout* L0 = reinterpret_cast<const rq_layout*>(mats + l0);
+  const rqio* io = reinterpret_cast<const rqio*>(mats + l0 + sizeof(rq_layout) / sizeof(cx));
+  uint64_t thr_ld = 0, thr_st = 0;  // this thread's chunk offsets in the load / store layout
+#pragma unroll
+  for (int k = 0; k < LOGNT; ++k) {
+    if ((t >> k) & 1u) {
+      thr_ld += io->gv_ld[k];
+      thr_st += io->gv_st[k];
+    }
+  }
+  const uint32_t tp0 = rq_tp<LOGNT>(L0, t);
+  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
+  const uint32_t count =
+      tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+  cx xf[RQ_R], xb[RQ_R];
+  for (uint32_t tt = 0; tt < count; ++tt) {
+    uint64_t base = (tile0 + tt) << fg.lc;
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
+    chunk* pf = f + (base + thr_ld);
+    chunk* pb = b + (base + thr_ld);
+    // per tile, so the compiler does not hold the offsets in SGPRs across the pass
+    uint32_t ro = l0;
+    asm volatile("" : "+s"(ro));
+    const rqio* rg = reinterpret_cast<const rqio*>(mats + ro + sizeof(rq_layout) / sizeof(cx));
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const chunk cf = ldc(pf + rg->offi_ld[i]);
+      xf[2 * i] = cf.v[0];
+      xf[2 * i + 1] = cf.v[1];
+      if constexpr (TWO) {
+        const chunk cb = ldc(pb + rg->offi_ld[i]);
+        xb[2 * i] = cb.v[0];
+        xb[2 * i + 1] = cb.v[1];
+      }
+    }
+    uint32_t tp = tp0;
+    const rq_layout* Lc = L0;
+    uint32_t ri = 0;
+    for (uint32_t j = 0; j < fg.nops; ++j) {
+      const fop op = ops[j];
+      const uint32_t kind = op.kind & 7u;
+      const bool gamma = TWO && (op.kind & FOP_GAMMA);
+      const cx* M = mats + op.mat;
+      real* acc = TWO ? &accw[wave][ri < FMAX_GRAD ? ri : 0][0] : nullptr;
+      if (kind == FK_RELAYOUT) {
+        const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
+        const uint32_t tpn = rq_tp<LOGNT>(Ln, t);
+        rq_exchange(xf, buf, tp, Lc, tpn, Ln);
+        if constexpr (TWO) rq_exchange(xb, buf, tp, Lc, tpn, Ln);
+        tp = tpn;
+        Lc = Ln;
+        continue;
+      }
+      // slot case (host: rq_plan): two-qubit / diagonal S1 * 4 + S2 (t1 in slot S1, t2 in
+      // slot S2); one-qubit: the slot of t1
+      switch (kind * 16u + op.t1) {
+        case FK_Q2 * 16 + 1: rq_q2<0, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 2: rq_q2<0, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 3: rq_q2<0, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 4: rq_q2<1, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 6: rq_q2<1, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 7: rq_q2<1, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 8: rq_q2<2, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 9: rq_q2<2, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 11: rq_q2<2, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 12: rq_q2<3, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 13: rq_q2<3, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q2 * 16 + 14: rq_q2<3, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 1: rq_diag<0, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 2: rq_diag<0, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 3: rq_diag<0, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 4: rq_diag<1, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 6: rq_diag<1, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 7: rq_diag<1, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 8: rq_diag<2, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 9: rq_diag<2, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 11: rq_diag<2, 3, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 12: rq_diag<3, 0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 13: rq_diag<3, 1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_DIAG * 16 + 14: rq_diag<3, 2, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q1 * 16 + 0: rq_q1<0, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q1 * 16 + 1: rq_q1<1, TWO>(xf, xb, M, gamma, acc); break;
+        case FK_Q1 * 16 + 2: rq_q1<2, TWO>(xf, xb, M, gamma, acc); break;
+        default: rq_q1<3, TWO>(xf, xb, M, gamma, acc); break;
+      }
+      if (gamma) ++ri;
+    }
+    // the program ends in the store layout.  The opaque redefinition keeps the compiler from
+    // holding the loads' 16 addresses across the pass.
+    pf = f + (base + thr_st);
+    pb = b + (base + thr_st);
+    asm volatile("" : "+v"(pf), "+v"(pb));
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      chunk c;
+      c.v[0] = xf[2 * i];
+      c.v[1] = xf[2 * i + 1];
+      stc(pf + rg->offi_st[i], c);
+      if constexpr (TWO) {
+        c.v[0] = xb[2 * i];
+        c.v[1] = xb[2 * i + 1];
+        stc(pb + rg->offi_st[i], c);
+      }
+    }
+  }
+  if constexpr (TWO) {
+    __syncthreads();
+    for (uint32_t i = t; i < fg.ngrad * FACC; i += NT) {
+      const uint32_t k = i / FACC, e = i % FACC;
+      real s = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) s += accw[w][k][e];
+      reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] = s;
+    }
+  }
+}
+#endif
+
+}  // namespace qdc

@@ -331,6 +331,28 @@ def fusion_schedule(qubits_number, instructions, mode, fwd_sens=None, precision=
     return ops, items
 
 
+def rq_plan(tile_bits, stages, deps=None, precision=None):
+    """The register-layout plan of a register-resident pass (qdc_rq_plan, host only).
+    stages = [(kind 0 one-qubit | 1 two-qubit | 2 diagonal, t1, t2)] in tile bits; deps[i] =
+    bit mask of the earlier stages stage i must follow.  Returns (load, steps, store): the
+    load / store layouts' slots and [{"relayout": bool, "stage": i, "case": c, "slots": [4]}]."""
+    lib = load(precision or default_precision())
+    n = len(stages)
+    kinds = (C.c_uint * max(n, 1))(*[int(s[0]) for s in stages])
+    t1 = (C.c_uint * max(n, 1))(*[int(s[1]) for s in stages])
+    t2 = (C.c_uint * max(n, 1))(*[int(s[2]) for s in stages])
+    dp = (C.c_ulonglong * max(n, 1))(*[int(d) for d in (deps or [0] * n)])
+    cap = 2 * n + 4
+    out = (C.c_uint * (7 * cap))()
+    k = int(lib.qdc_rq_plan(tile_bits, kinds, t1, t2, dp, n, out, cap))
+    if k == 2**64 - 1:
+        raise RuntimeError("rq plan output capacity exceeded")
+    rows = [[int(out[7 * i + j]) for j in range(7)] for i in range(k)]
+    steps = [{"relayout": r[0] == 1, "stage": r[1], "case": r[2], "slots": r[3:7]}
+             for r in rows[1:-1]]
+    return rows[0][3:7], steps, rows[-1][3:7]
+
+
 # ---------------------------------------------------------------------------------------
 # QuantizedTensor (src/quantized_tensor.rs:54-238) over the 18-function C ABI
 # ---------------------------------------------------------------------------------------

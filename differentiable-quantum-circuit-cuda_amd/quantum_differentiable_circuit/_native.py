@@ -33,6 +33,7 @@ RUNTIME = (
     "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
     "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_plan", "qdc_fusion_schedule",
+    "qdc_rq_plan",
 )
 
 
@@ -107,6 +108,9 @@ def _proto(lib):
                                      _S, C.POINTER(PlanOp), _S, C.c_int, C.c_int,
                                      C.POINTER(C.c_uint), _S, C.POINTER(C.c_uint), _S,
                                      C.POINTER(C.c_uint), _S]),
+        "qdc_rq_plan": (_S, [C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                             C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong), _S,
+                             C.POINTER(C.c_uint), _S]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

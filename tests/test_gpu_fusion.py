@@ -182,3 +182,58 @@ def test_fused_densities_with_nonunitary_matrices_on_unitary_kinds(prec):
     _, cots = O.tsallis_loss_and_cotangents([d.astype(np.complex128) for d in want])
     cots = [np.ascontiguousarray(x.conj(), dtype=dt) for x in cots]
     assert normrel(c.backward(cots, cg, vg), o.backward(cots, cg, vg)) < TOL[prec]
+
+
+def build_env(prec, n, ins, env):
+    import quantum_differentiable_circuit as q
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        c = q.circuit_class(prec)(n)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    return c
+
+
+@pytest.mark.parametrize("case", ["layered12", "layered16", "random12", "random17"])
+def test_register_resident_passes_equal_lds_passes(case):
+    """f32 gate passes run register-resident (k_rq, csrc/qdc_rq.hpp: relayouts through LDS,
+    stages on VGPRs) by default; QDC_RQ=0 keeps them in LDS tiles (k_fused).  Both must agree
+    with each other and with the oracle, forward and reverse sweep."""
+    dt = np.complex64
+    kind, n = case[:-2], int(case[-2:])
+    if kind == "layered":
+        ins, var = O.layered_circuit(n, 4, seed=24)
+        const = []
+        psi0 = None
+    else:
+        ins, const, var = O.random_circuit(n, 160, seed=200 + n, density_every=0)
+        psi0 = O.random_state(np.random.default_rng(n), n).astype(dt)
+    cg = [g.astype(dt) for g in const]
+    vg = [g.astype(dt) for g in var]
+    res = {}
+    for rq in (0, 1):
+        c = build_env("f32", n, ins, {"QDC_RQ": rq, "QDC_FUSE": 1})
+        if psi0 is not None:
+            c.set_state_from_vector(psi0)
+        d = c.forward(cg, vg)
+        cots = [np.diag([1.0, -1.0]).astype(dt) if x.shape == (2, 2)
+                else np.diag([1.0, -1.0, -1.0, 1.0]).astype(dt) for x in d]
+        res[rq] = (d, c.backward(cots, cg, vg), cots)
+    o = O.OracleCircuit(n, dt)
+    for k, pos in ins:
+        o.add(k, *pos)
+    if psi0 is not None:
+        o.set_state_from_vector(psi0)
+    want_d = o.forward(cg, vg)
+    want_g = o.backward(res[0][2], cg, vg)
+    for rq in (0, 1):
+        assert normrel(res[rq][0], want_d) < TOL["f32"], rq
+        assert normrel(res[rq][1], want_g) < TOL["f32"] * 10, rq
+    assert normrel(res[1][1], res[0][1]) < TOL["f32"]

@@ -30,7 +30,7 @@ def bench_name(kernel):
     m = re.search(r"k_diag<(\d+)", kernel)
     if m:
         return DIAG[int(m.group(1))]
-    m = re.search(r"k_fused<(true|false), \d+, (true|false), (true|false)>", kernel)
+    m = re.search(r"k_fused<(true|false), \d+, (true|false), (true|false)(?:, \d+)?>", kernel)
     if m:  # <TWO, TB, HASRED, WF> -> the bench's per-variant names
         two, wf = m.group(1) == "true", m.group(3) == "true"
         return ("fused_reverse" if wf else "fused_inject") if two else \
