@@ -317,8 +317,10 @@ def main():
                for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"])}
 
     # sanity: the loss gradient is finite and the densities are traces of 1
-    assert all(np.isfinite(g).all() for g in grads)
-    assert all(abs(np.trace(d) - 1) < 1e-3 for d in dens)
+    # (QDC_BENCH_ABLATION: timing-only builds that skip part of the kernel work)
+    if not os.environ.get("QDC_BENCH_ABLATION"):
+        assert all(np.isfinite(g).all() for g in grads)
+        assert all(abs(np.trace(d) - 1) < 1e-3 for d in dens)
 
     # the fused path against the per-gate roofline: every gate costs 2S forward and 4S in the
     # reverse sweep (SURVEY.md §8 d) if applied one HBM pass at a time

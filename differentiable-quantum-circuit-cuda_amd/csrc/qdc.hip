@@ -253,10 +253,11 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   std::vector<uint8_t> sens(n_instr, 0);
   if (inexact)
     for (size_t k = 0; k < n_instr; ++k) sens[k] = inexact[k] ? 1 : 0;
-  const qdc::FusionPlanner P{ins, sens, (uint32_t)local_qubits, true, true,
+  qdc::FusionPlanner P{ins, sens, (uint32_t)local_qubits, true, true,
                              max_ops > 0 ? (uint32_t)std::min(max_ops, qdc::FMAX_OPS)
                                          : (uint32_t)qdc::FMAX_OPS,
                              lcmin > 0 ? (uint32_t)lcmin : 3u};
+  if (const char* e = getenv("QDC_TILE2_CHUNKS")) P.tile2_chunks = (uint32_t)atoi(e);
   const std::vector<qdc_plan_op> pl(plan, plan + n_plan);
   const std::vector<qdc::FusionItem> items = P.fuse_items(pl, backward != 0, first_inject);
   size_t ns = 0, no = 0;

@@ -148,6 +148,8 @@ struct Circuit {
   int fuse_meas = 1;        // densities / cotangent injections join fused passes
   int use_rq = 1;           // f32 gate passes run register-resident (qdc_rq.hpp)
   int rq_stats = 0;
+  int rq_prefetch = 1;      // register-resident passes prefetch the next tile (QDC_RQ_PF)
+
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
@@ -178,6 +180,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_FUSE_MEAS")) fuse_meas = atoi(e);
     if (const char* e = getenv("QDC_RQ")) use_rq = atoi(e);
     if (const char* e = getenv("QDC_RQ_STATS")) rq_stats = atoi(e);
+    if (const char* e = getenv("QDC_RQ_PF")) rq_prefetch = atoi(e);
+
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
@@ -730,9 +734,12 @@ struct Circuit {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     const void* kern = nullptr;
-    if (two && nt == 128) kern = (const void*)k_rq<true, 128>;
-    else if (!two && nt == 128) kern = (const void*)k_rq<false, 128>;
-    else if (!two && nt == 256) kern = (const void*)k_rq<false, 256>;
+    // the next tile's prefetch pays in one-state passes only: two-state ones would double 64
+    // state VGPRs and drop to 2 waves/SIMD (measured 4 % slower at C2 n=28)
+    const bool pf = rq_prefetch != 0 && !two;
+    if (two && nt == 128) kern = (const void*)k_rq<true, 128, false>;
+    else if (!two && nt == 128) kern = pf ? (const void*)k_rq<false, 128, true> : (const void*)k_rq<false, 128, false>;
+    else if (!two && nt == 256) kern = pf ? (const void*)k_rq<false, 256, true> : (const void*)k_rq<false, 256, false>;
     else return fail("no register-resident kernel for a %u-amplitude %s tile", 1u << tbits,
                      two ? "two-state" : "one-state");
     uint32_t grid = 0;
@@ -744,14 +751,17 @@ struct Circuit {
     grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
-    if (two)
-      return ctx.launch_block(name, bytes, k_rq<true, 128>, grid, nt, f, b, fops, mats, g, l0,
-                              partials, stride);
-    if (nt == 128)
-      return ctx.launch_block(name, bytes, k_rq<false, 128>, grid, nt, f, b, fops, mats, g, l0,
-                              partials, stride);
-    return ctx.launch_block(name, bytes, k_rq<false, 256>, grid, nt, f, b, fops, mats, g, l0,
+#define QDC_RQ_LAUNCH(T, N, P)                                                            \
+  if (two == T && nt == N && pf == P)                                                     \
+    return ctx.launch_block(name, bytes, k_rq<T, N, P>, grid, nt, f, b, fops, mats, g, l0, \
                             partials, stride);
+    QDC_RQ_LAUNCH(true, 128, false)
+    QDC_RQ_LAUNCH(false, 128, true)
+    QDC_RQ_LAUNCH(false, 128, false)
+    QDC_RQ_LAUNCH(false, 256, true)
+    QDC_RQ_LAUNCH(false, 256, false)
+#undef QDC_RQ_LAUNCH
+    return fail("no register-resident kernel launched");
 #else
     (void)name; (void)bytes; (void)fg; (void)two; (void)tbits; (void)l0; (void)f; (void)b;
     (void)fops; (void)mats; (void)partials; (void)stride;

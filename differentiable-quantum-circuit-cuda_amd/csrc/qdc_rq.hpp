@@ -237,8 +237,14 @@ __device__ __forceinline__ void rq_exchange(cx (&x)[RQ_R], cx* buf, uint32_t tp,
 
 // TWO: fwd and bwd (reverse sweep, Gamma stages reduce into partials); else fwd only.
 // fg.nops ops at `ops`; at mats + l0 the load layout's descriptor, then rqio.
-template <bool TWO, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef QDC_RQ_PF_WAVES
+#define QDC_RQ_PF_WAVES 2  // waves/SIMD of the prefetching variant (state + next tile in VGPRs)
+#endif
+// PF: software pipeline — the next tile's chunks are loaded into registers while this tile's
+// stages run (2x the state registers, so fewer waves; no spills allowed: a scratch reload would
+// wait for the in-flight prefetch, vmcnt being in order).
+template <bool TWO, int NT, bool PF>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF ? QDC_RQ_PF_WAVES : 4)))
 void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
@@ -269,18 +275,23 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
   const uint32_t count =
       tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
-  cx xf[RQ_R], xb[RQ_R];
-  for (uint32_t tt = 0; tt < count; ++tt) {
-    uint64_t base = (tile0 + tt) << fg.lc;
+  auto tile_base = [&](uint64_t tile) {
+    uint64_t base = tile << fg.lc;
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    chunk* pf = f + (base + thr_ld);
-    chunk* pb = b + (base + thr_ld);
-    // per tile, so the compiler does not hold the offsets in SGPRs across the pass
+    return base;
+  };
+  // re-read per use, so the compiler does not hold the offsets in SGPRs across the pass
+  auto rqio_now = [&]() {
     uint32_t ro = l0;
     asm volatile("" : "+s"(ro));
-    const rqio* rg = reinterpret_cast<const rqio*>(mats + ro + sizeof(rq_layout) / sizeof(cx));
+    return reinterpret_cast<const rqio*>(mats + ro + sizeof(rq_layout) / sizeof(cx));
+  };
+  auto load = [&](cx (&xf)[RQ_R], cx (&xb)[RQ_R], uint64_t base) __attribute__((always_inline)) {
+    const rqio* rg = rqio_now();
+    const chunk* pf = f + (base + thr_ld);
+    const chunk* pb = b + (base + thr_ld);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const chunk cf = ldc(pf + rg->offi_ld[i]);
@@ -292,6 +303,28 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         xb[2 * i + 1] = cb.v[1];
       }
     }
+  };
+  // the program ends in the store layout.  The opaque redefinition keeps the compiler from
+  // holding the loads' 16 addresses across the pass.
+  auto store = [&](cx (&xf)[RQ_R], cx (&xb)[RQ_R], uint64_t base) __attribute__((always_inline)) {
+    const rqio* rg = rqio_now();
+    chunk* pf = f + (base + thr_st);
+    chunk* pb = b + (base + thr_st);
+    asm volatile("" : "+v"(pf), "+v"(pb));
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      chunk c;
+      c.v[0] = xf[2 * i];
+      c.v[1] = xf[2 * i + 1];
+      stc(pf + rg->offi_st[i], c);
+      if constexpr (TWO) {
+        c.v[0] = xb[2 * i];
+        c.v[1] = xb[2 * i + 1];
+        stc(pb + rg->offi_st[i], c);
+      }
+    }
+  };
+  auto run = [&](cx (&xf)[RQ_R], cx (&xb)[RQ_R]) __attribute__((always_inline)) {
     uint32_t tp = tp0;
     const rq_layout* Lc = L0;
     uint32_t ri = 0;
@@ -344,22 +377,34 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       }
       if (gamma) ++ri;
     }
-    // the program ends in the store layout.  The opaque redefinition keeps the compiler from
-    // holding the loads' 16 addresses across the pass.
-    pf = f + (base + thr_st);
-    pb = b + (base + thr_st);
-    asm volatile("" : "+v"(pf), "+v"(pb));
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      chunk c;
-      c.v[0] = xf[2 * i];
-      c.v[1] = xf[2 * i + 1];
-      stc(pf + rg->offi_st[i], c);
-      if constexpr (TWO) {
-        c.v[0] = xb[2 * i];
-        c.v[1] = xb[2 * i + 1];
-        stc(pb + rg->offi_st[i], c);
+  };
+  if constexpr (!PF) {
+    cx xf[RQ_R], xb[RQ_R];
+    for (uint32_t tt = 0; tt < count; ++tt) {
+      const uint64_t base = tile_base(tile0 + tt);
+      load(xf, xb, base);
+      run(xf, xb);
+      store(xf, xb, base);
+    }
+  } else {
+    // two register sets, ping-pong: tile tt+1 loads while tile tt runs
+    cx af[RQ_R], ab[RQ_R], bf[RQ_R], bb[RQ_R];
+    uint64_t base_a = count ? tile_base(tile0) : 0, base_b = 0;
+    if (count) load(af, ab, base_a);
+    for (uint32_t tt = 0; tt < count; tt += 2) {
+      if (tt + 1 < count) {
+        base_b = tile_base(tile0 + tt + 1);
+        load(bf, bb, base_b);
       }
+      run(af, ab);
+      store(af, ab, base_a);
+      if (tt + 1 >= count) break;
+      if (tt + 2 < count) {
+        base_a = tile_base(tile0 + tt + 2);
+        load(af, ab, base_a);
+      }
+      run(bf, bb);
+      store(bf, bb, base_b);
     }
   }
   if constexpr (TWO) {

@@ -35,6 +35,9 @@ def bench_name(kernel):
         two, wf = m.group(1) == "true", m.group(3) == "true"
         return ("fused_reverse" if wf else "fused_inject") if two else \
                ("fused_apply" if wf else "fused_density")
+    m = re.search(r"k_rq<(true|false), \d+(?:, (?:true|false))?>", kernel)
+    if m:  # register-resident gate passes (qdc_rq.hpp): <TWO, NT>
+        return "fused_reverse" if m.group(1) == "true" else "fused_apply"
     if "k_elementwise<0>" in kernel:
         return "copy"
     if "k_finalize" in kernel:
