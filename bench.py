@@ -188,6 +188,39 @@ def gate_kernel_sample(args, n):
     return out
 
 
+def dense_gate_sample(args, n):
+    """Dense k-qubit gates (k = 3, 4, 5; include/qdc/dense.h) on the matrix cores at n: 8
+    random unitaries per k at mixed positions, per-kernel HIP-event time on the primitives'
+    stream, algorithmic bytes 2S and FLOPs 8 * 2^k per amplitude."""
+    import quantum_differentiable_circuit as q
+    dt = np.complex64 if args.precision == "f32" else np.complex128
+    rng = np.random.default_rng(2)
+    t = q.QuantizedTensor.new_standard(n, precision=args.precision)
+    mats = {k: [np.ascontiguousarray(O_haar(rng, 1 << k), dtype=dt) for _ in range(8)]
+            for k in (3, 4, 5)}
+    poss = {k: [list(rng.permutation(n)[:k]) for _ in range(8)] for k in (3, 4, 5)}
+    for k in (3, 4, 5):  # warm-up
+        t.apply_qk_gate(mats[k][0], poss[k][0])
+    q.primitives_sync(args.precision)
+    q.primitives_profile(True, args.precision)
+    for k in (3, 4, 5):
+        for u, pos in zip(mats[k], poss[k]):
+            t.apply_qk_gate(u, pos)
+    stats = q.primitives_profile_collect(args.precision)
+    q.primitives_profile(False, args.precision)
+    del t
+    out = {}
+    for k in (3, 4, 5):
+        s = stats.get(f"qk{k}")
+        if s and s["total_ms"] > 0:
+            gbs = s["algo_bytes"] / (s["total_ms"] * 1e-3) / 1e9
+            out[f"qk{k}"] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                             "TFLOP/s": round(s["algo_flops"] / (s["total_ms"] * 1e-3) / 1e12, 2),
+                             "launches": s["launches"],
+                             "avg_ms": round(s["total_ms"] / s["launches"], 4)}
+    return out
+
+
 def micro(args):
     """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse
     (single-gate kernels: fusion off)."""
@@ -328,9 +361,10 @@ def main():
     eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / max(world, 1)
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
-    gate_kernels = None
+    gate_kernels = dense_kernels = None
     if rank == 0 and world == 1 and not args.no_gate_sample:
         gate_kernels = gate_kernel_sample(args, n)
+        dense_kernels = dense_gate_sample(args, n)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -375,6 +409,7 @@ def main():
             "kernels": kernels,
             "effective_gate_bandwidth": effective,
             "gate_kernels": gate_kernels,
+            "dense_gate_kernels": dense_kernels,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -211,27 +211,7 @@ QDC_API const char* qdc_circuit_profile(qdc_circuit* c, int on) {
 }
 
 QDC_API size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out, size_t cap) {
-  qdc::Ctx& x = c->impl.ctx;
-  (void)hipStreamSynchronize(x.stream);
-  std::vector<qdc_kernel_stat> agg;
-  for (auto& r : x.prof.recs) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = 0.f;
-    qdc_kernel_stat* s = nullptr;
-    for (auto& a : agg)
-      if (strncmp(a.name, r.name, sizeof(a.name)) == 0) s = &a;
-    if (!s) {
-      agg.push_back({});
-      s = &agg.back();
-      strncpy(s->name, r.name, sizeof(s->name) - 1);
-    }
-    s->launches += 1;
-    s->total_ms += ms;
-    s->algo_bytes += r.bytes;
-    s->algo_flops += r.flops;
-  }
-  for (size_t i = 0; i < agg.size() && i < cap; ++i) out[i] = agg[i];
-  return agg.size();
+  return qdc::prof_collect(c->impl.ctx, out, cap);
 }
 
 QDC_API const char* qdc_build_info(void) {
@@ -258,6 +238,7 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
                                          : (uint32_t)qdc::FMAX_OPS,
                              lcmin > 0 ? (uint32_t)lcmin : 3u};
   if (const char* e = getenv("QDC_TILE2_CHUNKS")) P.tile2_chunks = (uint32_t)atoi(e);
+  if (const char* e = getenv("QDC_TILE1_CHUNKS")) P.tile1_chunks = (uint32_t)atoi(e);
   const std::vector<qdc_plan_op> pl(plan, plan + n_plan);
   const std::vector<qdc::FusionItem> items = P.fuse_items(pl, backward != 0, first_inject);
   size_t ns = 0, no = 0;

@@ -69,7 +69,8 @@ struct FusionPlanner {
   bool fuse_meas;
   uint32_t fuse_max_ops;
   uint32_t fuse_lcmin;
-  uint32_t tile2_chunks = TILE_CHUNKS_2;  // two-state tile (register-resident passes: 2048)
+  uint32_t tile2_chunks = TILE_CHUNKS_2;  // two-state tile (chunks per state)
+  uint32_t tile1_chunks = TILE_CHUNKS_1;  // one-state tile
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -146,7 +147,7 @@ struct FusionPlanner {
   std::vector<FusionItem> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
                                size_t first_inject = SIZE_MAX) const {
     std::vector<FusionItem> items;
-    const uint32_t T = log2_of(backward ? tile2_chunks : TILE_CHUNKS_1);
+    const uint32_t T = log2_of(backward ? tile2_chunks : tile1_chunks);
     const bool on = fuse && fuse_max_ops >= 2;
     auto fusable = [&](size_t k) {
       const qdc_plan_op& op = plan[k];

@@ -7,7 +7,10 @@
 // safe (the reference's are not, README.md:13).
 #pragma once
 
+#include "qdc/circuit.h"
+#include "qdc/dense.h"
 #include "qdc_device.hpp"
+#include "qdc_qk.hpp"
 
 namespace qdc {
 
@@ -49,6 +52,31 @@ inline const char* abi_finish_reduction(Ctx& c, qdc_complex* out, int K) {
     out[k].im += c.host_results[k].y;
   }
   return nullptr;
+}
+
+// per-kernel sums of a context's profiled launches (qdc_circuit_profile_collect,
+// qdc_abi_profile_collect)
+inline size_t prof_collect(Ctx& x, qdc_kernel_stat* out, size_t cap) {
+  (void)hipStreamSynchronize(x.stream);
+  std::vector<qdc_kernel_stat> agg;
+  for (auto& r : x.prof.recs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = 0.f;
+    qdc_kernel_stat* s = nullptr;
+    for (auto& a : agg)
+      if (strncmp(a.name, r.name, sizeof(a.name)) == 0) s = &a;
+    if (!s) {
+      agg.push_back({});
+      s = &agg.back();
+      strncpy(s->name, r.name, sizeof(s->name) - 1);
+    }
+    s->launches += 1;
+    s->total_ms += ms;
+    s->algo_bytes += r.bytes;
+    s->algo_flops += r.flops;
+  }
+  for (size_t i = 0; i < agg.size() && i < cap; ++i) out[i] = agg[i];
+  return agg.size();
 }
 
 }  // namespace qdc
@@ -259,6 +287,52 @@ __attribute__((visibility("default"))) void add(const qdc_complex* src, qdc_comp
 __attribute__((visibility("default"))) void copy(const qdc_complex* src, qdc_complex* dst,
                                                  size_t n) {
   QDC_VOID(elementwise_impl<0>(src, dst, n));
+}
+
+// ---- extensions beyond the reference's 18 entry points (include/qdc/dense.h) ----------------
+
+__attribute__((visibility("default"))) const char* qdc_qkgate(qdc_complex* state,
+                                                              const qdc_complex* gate,
+                                                              const size_t* pos, size_t k,
+                                                              size_t n) {
+  QDC_ABI_BEGIN
+  QDC_TRY(qdc::check_n(n));
+  if (k < 1 || k > (size_t)qdc::QK_MAX)
+    return qdc::fail("k = %zu qubits is out of the supported range (1..%d).", k, qdc::QK_MAX);
+  if (k > n) return qdc::fail("k = %zu exceeds qubits_number %zu.", k, n);
+  for (size_t b = 0; b < k; ++b) {
+    if (pos[b] >= n) return qdc::fail("pos is out of the bound.");
+    for (size_t c = 0; c < b; ++c)
+      if (pos[c] == pos[b]) return qdc::fail("positions must be different.");
+  }
+  static qdc::real* buf = nullptr;  // guarded by the ABI mutex
+  static size_t cap = 0;
+  return qdc::apply_qk(ctx, reinterpret_cast<qdc::cx*>(state), gate, pos, (uint32_t)k,
+                       (uint32_t)n, buf, cap);
+}
+
+__attribute__((visibility("default"))) const char* qdc_abi_sync(void) {
+  QDC_ABI_BEGIN
+  QDC_HIP(hipStreamSynchronize(ctx.stream));
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) const char* qdc_abi_profile(int on) {
+  QDC_ABI_BEGIN
+  if (on) {
+    QDC_HIP(hipStreamSynchronize(ctx.stream));
+    ctx.prof.reset();
+  }
+  ctx.prof.on = on != 0;
+  return nullptr;
+}
+
+__attribute__((visibility("default"))) size_t qdc_abi_profile_collect(qdc_kernel_stat* out,
+                                                                      size_t cap) {
+  std::lock_guard<std::mutex> lock(qdc::abi_mutex());
+  qdc::Ctx* c = nullptr;
+  if (qdc::abi_ctx(c)) return 0;
+  return qdc::prof_collect(*c, out, cap);
 }
 
 }  // extern "C"

@@ -1,0 +1,171 @@
+// qdc_qk.hpp — dense k-qubit gates (k = 3..5) on MFMA (SURVEY.md §8 f rank 4; outside the
+// reference's API, which stops at 2-qubit gates).
+//
+// A k-qubit gate maps each group of C = 2^k amplitudes (indices that differ only in the target
+// bits) through a C×C complex matrix: out[r] = sum_c U[r*C + c] in[c], local index bit (k-1-b)
+// = qubit pos[b] (pos[0] is the most significant, like q2gate's pos2, primitives.cu:573-620).
+// In real form that is a 2C×2C matrix applied to 2^(n-k) vectors of 2C reals: a batched GEMM
+// with 4C real MACs per amplitude (k=3: 32, k=5: 128), so at k >= 3 it is a real contraction
+// and runs on the matrix cores: v_mfma_{f32,f64}_16x16x4 with the gate as the A operand
+// (resident in VGPRs for the whole kernel) and 16 groups per instruction as the B operand.
+//
+// Operand mapping (16x16x4: A[i][kk] in lane kk*16 + i; B[kk][j] in lane kk*16 + j; D row i,
+// column j in lane a*16 + j, register r, with i = 4a + r for f32 and i = 4r + a for f64).  Lane l = q*16 + j owns group j of the batch and
+// its amplitudes c = (C/4) q + m, m < C/4 (both parts) — it loads them, and gets exactly them
+// back in D, so the kernel is lane-local in place:
+//   K step s (C/2 per output tile) reads B = part (s % 2) of amplitude (C/4) kk + s/2;
+//   output tile t (C/8 of them): lane group a, register r = part (r % 2) of amplitude
+//   (C/4) a + 2t + r/2 (qk_operands orders the gate's rows to match).
+// The host forms each lane's A values (qk_operands) once per call.
+#pragma once
+
+#include "qdc_device.hpp"
+
+namespace qdc {
+
+constexpr int QK_MAX = 5;
+
+struct qk_geo {
+  uint64_t off[1 << QK_MAX];  // amplitude offset of local index c from the group base
+  uint32_t sorted[QK_MAX];    // target positions, ascending (group base: insert zeros)
+  uint32_t k;
+  uint64_t ngroups;
+};
+
+// lane l's A operand for (tile t, K step s), at [(t * C/2 + s) * 64 + l]
+template <int K>
+inline void qk_operands(const cx* U, std::vector<real>& a) {
+  constexpr int C = 1 << K;
+  a.assign((size_t)(C / 8) * (C / 2) * 64, 0);
+  for (int t = 0; t < C / 8; ++t)
+    for (int s = 0; s < C / 2; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int i = l % 16, kk = l / 16;
+        // D row i sits in lane group ga, register r: f32 i = 4 ga + r; f64 i = 4 r + ga
+        // (probed: tools/mfma_layout_probe.hip, tools/mfma_f64_layout_probe.hip)
+#ifdef QDC_F64
+        const int ga = i % 4, r = i / 4;
+#else
+        const int ga = i / 4, r = i % 4;
+#endif
+        const int ro = (C / 4) * ga + 2 * t + r / 2, po = r % 2;
+        const int ci = (C / 4) * kk + s / 2, pi = s % 2;
+        const cx u = U[ro * C + ci];
+        // [Re -Im; Im Re] acting on (re, im)
+        const real v = po == 0 ? (pi == 0 ? u.x : -u.y) : (pi == 0 ? u.y : u.x);
+        a[((size_t)t * (C / 2) + s) * 64 + l] = v;
+      }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __restrict__ aop,
+                                            qk_geo g) {
+  constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
+#ifdef QDC_F64
+  using acc_t = double __attribute__((ext_vector_type(4)));
+#else
+  using acc_t = float __attribute__((ext_vector_type(4)));
+#endif
+  const int l = threadIdx.x & 63;
+  const int q = l >> 4, j = l & 15;
+  real a[T][S];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int u = 0; u < S; ++u) a[t][u] = aop[((size_t)t * S + u) * 64 + l];
+  uint64_t off[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) off[m] = g.off[M * q + m];
+  // NB batches of 16 groups per iteration, all loads first (bytes in flight per wave)
+  constexpr int NB = K == 3 ? 4 : K == 4 ? 2 : 1;
+  const uint64_t nbatch = (g.ngroups + 15) / 16;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t bt0 = wave * NB; bt0 < nbatch; bt0 += nwaves * NB) {
+    uint64_t base[NB];
+    bool live[NB];
+    cx x[NB][M];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const uint64_t grp = (bt0 + nb) * 16 + (uint64_t)j;
+      live[nb] = grp < g.ngroups;
+      base[nb] = grp;
+#pragma unroll
+      for (int b = 0; b < K; ++b) base[nb] = insert_zero(base[nb], g.sorted[b]);
+#pragma unroll
+      for (int m = 0; m < M; ++m) x[nb][m] = live[nb] ? s[base[nb] + off[m]] : cx{0, 0};
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        acc_t d = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+          const real bv = (u & 1) ? x[nb][u >> 1].y : x[nb][u >> 1].x;
+#ifdef QDC_F64
+          d = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][u], bv, d, 0, 0, 0);
+#else
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u], bv, d, 0, 0, 0);
+#endif
+        }
+        if (live[nb]) {
+          s[base[nb] + off[2 * t]] = cx{d[0], d[1]};
+          s[base[nb] + off[2 * t + 1]] = cx{d[2], d[3]};
+        }
+      }
+    }
+  }
+}
+
+}  // namespace qdc
+
+namespace qdc {
+
+// Dense k-qubit gate on a state (k = 1, 2 route to the single-gate kernels).  `U` is the
+// host gate (C×C row-major), `pos` the k target qubits (pos[0] most significant).  The
+// operand buffer is device memory owned by the caller, grown here; the call synchronises the
+// stream around its upload (the reference uploads every gate with cudaMemcpyToSymbol too).
+inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* pos, uint32_t k,
+                            uint32_t n, real*& buf, size_t& cap) {
+  if (k == 1) return apply_dense<2>(c, s, to_mat<2>(U), (uint32_t)pos[0], (uint32_t)pos[0], n, "qk1");
+  if (k == 2)
+    return apply_dense<4>(c, s, to_mat<4>(U), (uint32_t)pos[0], (uint32_t)pos[1], n, "qk2");
+  const uint32_t C = 1u << k;
+  std::vector<cx> u(C * C);
+  for (uint32_t i = 0; i < C * C; ++i) u[i] = cx{(real)U[i].re, (real)U[i].im};
+  std::vector<real> a;
+  if (k == 3) qk_operands<3>(u.data(), a);
+  else if (k == 4) qk_operands<4>(u.data(), a);
+  else qk_operands<5>(u.data(), a);
+  qk_geo g{};
+  g.k = k;
+  g.ngroups = (uint64_t)1 << (n - k);
+  for (uint32_t b = 0; b < k; ++b) g.sorted[b] = (uint32_t)pos[b];
+  std::sort(g.sorted, g.sorted + k);
+  for (uint32_t ci = 0; ci < C; ++ci) {
+    uint64_t o = 0;
+    for (uint32_t b = 0; b < k; ++b)
+      if ((ci >> (k - 1 - b)) & 1u) o |= (uint64_t)1 << pos[b];
+    g.off[ci] = o;
+  }
+  QDC_HIP(hipStreamSynchronize(c.stream));  // the previous qk launch is done with buf
+  if (a.size() > cap) {
+    if (buf) QDC_HIP(hipFree(buf));
+    buf = nullptr;
+    QDC_HIP(hipMalloc(&buf, a.size() * sizeof(real)));
+    cap = a.size();
+  }
+  QDC_HIP(hipMemcpyAsync(buf, a.data(), a.size() * sizeof(real), hipMemcpyHostToDevice, c.stream));
+  QDC_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t nb = k == 3 ? 4 : k == 4 ? 2 : 1;  // batches per wave iteration (k_qk)
+  const uint64_t waves = ((g.ngroups + 15) / 16 + nb - 1) / nb;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 256u * 16u);
+  c.next_flops = 8.0 * C * (double)((uint64_t)1 << n);  // C complex MACs per amplitude
+  const double bytes = 2.0 * state_bytes(n);
+  if (k == 3) return c.launch_block("qk3", bytes, k_qk<3>, grid, 256u, s, buf, g);
+  if (k == 4) return c.launch_block("qk4", bytes, k_qk<4>, grid, 256u, s, buf, g);
+  return c.launch_block("qk5", bytes, k_qk<5>, grid, 256u, s, buf, g);
+}
+
+}  // namespace qdc

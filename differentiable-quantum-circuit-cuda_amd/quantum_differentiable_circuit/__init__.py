@@ -232,6 +232,28 @@ class _CircuitBase:
                 for i in range(min(k, cap))}
 
 
+def primitives_sync(precision=None):
+    """Wait for the primitives' stream (qdc_abi_sync, include/qdc/dense.h)."""
+    check(load(precision or default_precision()).qdc_abi_sync())
+
+
+def primitives_profile(on: bool, precision=None):
+    """Per-launch HIP-event profiling of the primitives' stream (qdc_abi_profile)."""
+    check(load(precision or default_precision()).qdc_abi_profile(1 if on else 0))
+
+
+def primitives_profile_collect(precision=None):
+    lib = load(precision or default_precision())
+    cap = 64
+    buf = (KernelStat * cap)()
+    k = int(lib.qdc_abi_profile_collect(buf, cap))
+    return {buf[i].name.decode(): {"launches": int(buf[i].launches),
+                                    "total_ms": float(buf[i].total_ms),
+                                    "algo_bytes": float(buf[i].algo_bytes),
+                                    "algo_flops": float(buf[i].algo_flops)}
+            for i in range(min(k, cap))}
+
+
 class Circuit32(_CircuitBase):
     """Single-precision build (complex64), like `maturin develop --release`."""
     _precision = "f32"
@@ -459,6 +481,22 @@ class QuantizedTensor:
         g = self._gate(gate, 16)
         self._pos2(pos2, pos1)
         check(self._lib.q2gate(self._p, ptr(g), pos2, pos1, self.qubits_number))
+
+    def apply_qk_gate(self, gate, positions):
+        """Dense k-qubit gate, 1 <= k <= 5 (include/qdc/dense.h; beyond the reference, whose
+        gates stop at 2 qubits): gate is 2^k x 2^k row-major, local index bit (k-1-b) is
+        qubit positions[b] (positions[0] most significant, as apply_q2_gate's pos2)."""
+        pos = [int(p) for p in positions]
+        k = len(pos)
+        if not 1 <= k <= 5:
+            raise PanicException("k must be in 1..5.")
+        g = self._gate(gate, 1 << (2 * k))
+        if len(set(pos)) != k:
+            raise PanicException("positions must be different.")
+        if max(pos) >= self.qubits_number:
+            raise PanicException("pos is out of the bound.")
+        arr = (C.c_size_t * k)(*pos)
+        check(self._lib.qdc_qkgate(self._p, ptr(g), arr, k, self.qubits_number))
 
     def apply_q2_gate_inv(self, gate, pos2, pos1):
         g = self._gate(gate, 16)

@@ -33,7 +33,7 @@ RUNTIME = (
     "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
     "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_plan", "qdc_fusion_schedule",
-    "qdc_rq_plan",
+    "qdc_rq_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
 )
 
 
@@ -108,6 +108,10 @@ def _proto(lib):
                                      _S, C.POINTER(PlanOp), _S, C.c_int, C.c_int,
                                      C.POINTER(C.c_uint), _S, C.POINTER(C.c_uint), _S,
                                      C.POINTER(C.c_uint), _S]),
+        "qdc_qkgate": (_E, [_P, _P, C.POINTER(C.c_size_t), _S, _S]),
+        "qdc_abi_sync": (_E, []),
+        "qdc_abi_profile": (_E, [C.c_int]),
+        "qdc_abi_profile_collect": (_S, [C.POINTER(KernelStat), _S]),
         "qdc_rq_plan": (_S, [C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                              C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong), _S,
                              C.POINTER(C.c_uint), _S]),

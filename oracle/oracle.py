@@ -77,6 +77,22 @@ def apply_q2_gate_diag(state, gate, pos2, pos1):
     return np.einsum("ijklm,lj->ijklm", s, g).reshape(-1)
 
 
+def apply_qk_gate(state, gate, positions):
+    """Dense k-qubit gate (include/qdc/dense.h; no reference counterpart — the convention
+    extends apply_q2_gate's: local index bit (k-1-b) is qubit positions[b], positions[0] the
+    most significant).  Parity unpinned beyond k = 2, where it must equal apply_q2_gate
+    (tests/test_oracle.py checks that)."""
+    n = qubits_of(state.size)
+    k = len(positions)
+    psi = np.asarray(state).reshape([2] * n)  # axis a = qubit n-1-a
+    u = np.asarray(gate).reshape([2] * (2 * k))  # out bits then in bits, MSB first
+    axes = [n - 1 - p for p in positions]
+    out = np.tensordot(u, psi, axes=(list(range(k, 2 * k)), axes))
+    # out axes: the k gate outputs (positions order), then psi's other axes in order
+    rest = [a for a in range(n) if a not in axes]
+    return np.transpose(out, np.argsort(axes + rest)).reshape(-1)
+
+
 def get_q1_density(state, pos):
     """quantized_tensor.rs:324-332: rho[2q+p] = sum psi[q] conj(psi[p])."""
     n = qubits_of(state.size)

@@ -222,3 +222,21 @@ def test_golden_circuits_reproduced(name, prec):
     cots = [c.reshape(int(np.sqrt(c.size)), -1) for c in split(z["cotangents"], z["cotangent_lens"])]
     grads = np.concatenate(o.backward(cots, const, var))
     assert np.abs(grads - z["grads"]).max() <= 1e-5 * np.abs(z["grads"]).max()
+
+
+def test_qk_oracle_extends_q1_q2_conventions():
+    """apply_qk_gate (dense k-qubit gates, include/qdc/dense.h) has no reference counterpart:
+    pin it to the reference's own q1/q2 oracles at k = 1, 2 and to a Kronecker product of
+    one-qubit gates (positions[0] = most significant factor) at k = 3."""
+    rng = np.random.default_rng(0)
+    n = 7
+    psi = O.random_state(rng, n)
+    for p2, p1 in ((5, 2), (1, 6), (0, 3)):
+        g = O.haar_unitary(rng, 4)
+        assert np.abs(O.apply_q2_gate(psi, g, p2, p1) - O.apply_qk_gate(psi, g, [p2, p1])).max() < 1e-14
+    g1 = O.haar_unitary(rng, 2)
+    assert np.abs(O.apply_q1_gate(psi, g1, 3) - O.apply_qk_gate(psi, g1, [3])).max() < 1e-14
+    a, b, c = (O.haar_unitary(rng, 2) for _ in range(3))
+    u = np.kron(np.kron(a.reshape(2, 2), b.reshape(2, 2)), c.reshape(2, 2))
+    want = O.apply_q1_gate(O.apply_q1_gate(O.apply_q1_gate(psi, a, 4), b, 0), c, 6)
+    assert np.abs(O.apply_qk_gate(psi, u.reshape(-1), [4, 0, 6]) - want).max() < 1e-14
