@@ -239,7 +239,9 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
                              lcmin > 0 ? (uint32_t)lcmin : 3u};
   if (const char* e = getenv("QDC_TILE2_CHUNKS")) P.tile2_chunks = (uint32_t)atoi(e);
   if (const char* e = getenv("QDC_TILE1_CHUNKS")) P.tile1_chunks = (uint32_t)atoi(e);
-  const std::vector<qdc_plan_op> pl(plan, plan + n_plan);
+  // the runtime's f32 register-resident settings (qdc_circuit.hpp planner())
+  if (const char* e = getenv("QDC_SCHED_RQ")) P.permute = P.rq_grad = atoi(e) != 0;
+  std::vector<qdc_plan_op> pl(plan, plan + n_plan);
   const std::vector<qdc::FusionItem> items = P.fuse_items(pl, backward != 0, first_inject);
   size_t ns = 0, no = 0;
   for (size_t i = 0; i < items.size(); ++i) {

@@ -149,6 +149,8 @@ struct Circuit {
   int use_rq = 1;           // f32 gate passes run register-resident (qdc_rq.hpp)
   int rq_stats = 0;
   int rq_prefetch = 1;      // register-resident passes prefetch the next tile (QDC_RQ_PF)
+  int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
+  int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -181,6 +183,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ")) use_rq = atoi(e);
     if (const char* e = getenv("QDC_RQ_STATS")) rq_stats = atoi(e);
     if (const char* e = getenv("QDC_RQ_PF")) rq_prefetch = atoi(e);
+    if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
+    if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -385,10 +389,15 @@ struct Circuit {
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
   static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
   FusionPlanner planner() const {
-    return FusionPlanner{ins, inexact, nl, fuse != 0, fuse_meas != 0, fuse_max_ops, fuse_lcmin};
+    FusionPlanner P{ins, inexact, nl, fuse != 0, fuse_meas != 0, fuse_max_ops, fuse_lcmin};
+    // gate-only passes permute their tile on the way out when they are register-resident
+    // (single-device layout only: the sharded remap planner owns the layout there)
+    P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
+    P.rq_grad = rq_grad32 && use_rq && sizeof(real) == 4;
+    return P;
   }
   bool is_meas(const qdc_plan_op& op) const { return planner().is_meas(op); }
-  std::vector<Item> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
+  std::vector<Item> fuse_items(std::vector<qdc_plan_op>& plan, bool backward,
                                size_t first_inject = SIZE_MAX) const {
     std::vector<Item> items;
     for (FusionItem& f : planner().fuse_items(plan, backward, first_inject)) {
@@ -646,6 +655,8 @@ struct Circuit {
       bool rq = use_rq && sizeof(real) == 4 && it.writes_f;
       for (const fop& F : pf) rq = rq && (F.kind & 7u) <= FK_DIAG;
       it.rq = rq;
+      if (!it.swaps.empty() && !rq)
+        return fail("internal: a permuting fused pass is not register-resident");
       it.tbits = (uint32_t)LV + it.lc + it.h;
       if (!rq) {
         for (const fop& F : pf) fops[fo++] = F;
@@ -668,12 +679,26 @@ struct Circuit {
             r.deps |= 1ull << i;
         rs.push_back(r);
       }
-      const RqPlan P = rq_plan(rs, it.tbits);
+      // a permuting pass: tile bit t's value is stored where tile bit dest[t] sits
+      uint32_t dest[32], src[4] = {0, 1, 2, 3};
+      const bool perm = !it.swaps.empty();
+      if (perm) {
+        for (uint32_t t = 0; t < it.tbits; ++t) {
+          uint32_t p = t < (uint32_t)LV + it.lc ? t : (uint32_t)LV + it.hb[t - LV - it.lc];
+          for (const auto& sw : it.swaps) {
+            if (p == sw.first) p = sw.second;
+            else if (p == sw.second) p = sw.first;
+          }
+          dest[t] = local_bit(p);
+          if (dest[t] < 4) src[dest[t]] = t;
+        }
+      }
+      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr);
       it.l0 = put_layout(P.load);
       {  // rqio after the load descriptor
         rqio io{};
         rq_hbm(P.load, it.tbits, it.lc, it.hb, io.gv_ld, io.offi_ld);
-        rq_hbm(P.store, it.tbits, it.lc, it.hb, io.gv_st, io.offi_st);
+        rq_hbm(P.store, it.tbits, it.lc, it.hb, io.gv_st, io.offi_st, perm ? dest : nullptr);
         std::memcpy(&mats[mo], &io, sizeof io);
         mo += sizeof(rqio) / sizeof(cx);
       }
@@ -839,6 +864,8 @@ struct Circuit {
       if (fg.ngrad > 0)
         for (uint32_t slot : it.grad_slots) ctx.commit(slot, last_fused_grid);
     }
+    // a permuting pass stored its tile's qubits at new positions (later ops were planned so)
+    for (const auto& sw : it.swaps) layout.swap_phys(sw.first, sw.second);
     return nullptr;
   }
 
@@ -888,7 +915,7 @@ struct Circuit {
           out_idx[k] = o++;
     }
     mark_inexact(cg, vg, gidx);
-    const std::vector<qdc_plan_op> pl = plan(mode);
+    std::vector<qdc_plan_op> pl = plan(mode);
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
     QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
@@ -971,7 +998,7 @@ struct Circuit {
     }
     bool have_bwd = false;
     mark_inexact(cg, vg, gidx);
-    const std::vector<qdc_plan_op> pl = plan(QDC_PLAN_BACKWARD);
+    std::vector<qdc_plan_op> pl = plan(QDC_PLAN_BACKWARD);
     size_t first_inject = pl.size();
     for (size_t i = 0; i < pl.size(); ++i)
       if (pl[i].type == QDC_PLAN_OP && is_diff_density(ins[pl[i].instr].kind)) {

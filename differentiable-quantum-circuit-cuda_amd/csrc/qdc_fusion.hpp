@@ -57,6 +57,9 @@ struct FusionItem {
   int type;
   std::vector<uint32_t> ops;  // plan indices, in execution order for type 2 passes
   uint32_t lc = 0, h = 0, hb[FMAX_ROWS] = {};
+  // physical qubit swaps the pass applies on its way out (its store writes the permuted
+  // layout; later ops' positions are already rewritten), in order
+  std::vector<std::pair<uint32_t, uint32_t>> swaps;
 };
 
 struct FusionPlanner {
@@ -71,6 +74,13 @@ struct FusionPlanner {
   uint32_t fuse_lcmin;
   uint32_t tile2_chunks = TILE_CHUNKS_2;  // two-state tile (chunks per state)
   uint32_t tile1_chunks = TILE_CHUNKS_1;  // one-state tile
+  // Gate-only passes may permute the qubits of their tile on the way out (register-resident
+  // passes store through any layout): the qubits the next ops need first move to the low
+  // physical positions 0..LV+2 that every tile holds, so later tiles are not spent on pinned
+  // qubits no op of theirs needs.
+  bool permute = false;
+  // two-state gate passes run register-resident (k_rq: FMAX_GRAD_RQ Gamma accumulators)
+  bool rq_grad = false;
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -144,8 +154,59 @@ struct FusionPlanner {
   }
 
   // backward: plan indices >= first_inject run two-state (bwd exists); a pass never spans it.
-  std::vector<FusionItem> fuse_items(const std::vector<qdc_plan_op>& plan, bool backward,
-                               size_t first_inject = SIZE_MAX) const {
+  // The low physical positions every tile holds: amplitude bits 0..LV-1 and chunk bits 0..2.
+  static constexpr uint32_t NLOW = (uint32_t)LV + 3;
+  // Choose the pass's swaps: rank the tile's qubits by the first upcoming op (`rest` of this
+  // segment, then plan[next..]) that uses them; the first NLOW move to the low positions.
+  void permute_after(FusionItem& it, std::vector<qdc_plan_op>& plan,
+                     const std::vector<uint32_t>& rest, size_t next) const {
+    std::vector<uint8_t> in_tile(nl, 0);
+    for (uint32_t p = 0; p < (uint32_t)LV + it.lc; ++p) in_tile[p] = 1;
+    for (uint32_t r = 0; r < it.h; ++r) in_tile[LV + it.hb[r]] = 1;
+    std::vector<uint32_t> want;
+    std::vector<uint8_t> ranked(nl, 0);
+    auto see = [&](const qdc_plan_op& op) {
+      if (op.type != QDC_PLAN_OP) return;
+      for (uint32_t p : {op.pos2, op.pos1})
+        if (p < nl && in_tile[p] && !ranked[p] && want.size() < NLOW) {
+          ranked[p] = 1;
+          want.push_back(p);
+        }
+    };
+    for (uint32_t k : rest) see(plan[k]);
+    for (size_t k = next; k < plan.size() && want.size() < NLOW; ++k) {
+      if (plan[k].type == QDC_PLAN_REMAP) break;
+      see(plan[k]);
+    }
+    std::vector<uint32_t> free_low;  // low positions whose qubit is not wanted
+    for (uint32_t p = 0; p < NLOW; ++p)
+      if (!ranked[p]) free_low.push_back(p);
+    size_t f = 0;
+    for (uint32_t p : want)
+      if (p >= NLOW) it.swaps.push_back({p, free_low[f++]});
+    if (it.swaps.empty()) return;
+    auto moved = [&](uint32_t p) {
+      for (const auto& sw : it.swaps) {
+        if (p == sw.first) p = sw.second;
+        else if (p == sw.second) p = sw.first;
+      }
+      return p;
+    };
+    for (uint32_t k : rest) {
+      plan[k].pos2 = moved(plan[k].pos2);
+      plan[k].pos1 = moved(plan[k].pos1);
+    }
+    for (size_t k = next; k < plan.size(); ++k) {
+      if (plan[k].type != QDC_PLAN_OP) continue;
+      plan[k].pos2 = moved(plan[k].pos2);
+      plan[k].pos1 = moved(plan[k].pos1);
+    }
+  }
+
+  // With `permute`, a fused gate-only pass gets `swaps` and the positions of every later op of
+  // `plan` are rewritten to the permuted layout.
+  std::vector<FusionItem> fuse_items(std::vector<qdc_plan_op>& plan, bool backward,
+                                     size_t first_inject = SIZE_MAX) const {
     std::vector<FusionItem> items;
     const uint32_t T = log2_of(backward ? tile2_chunks : tile1_chunks);
     const bool on = fuse && fuse_max_ops >= 2;
@@ -174,6 +235,7 @@ struct FusionPlanner {
              !(backward && j == first_inject && j > i))
         ++j;
       const bool two = backward && i >= first_inject;
+      const uint32_t gmax = (two && rq_grad) ? (uint32_t)FMAX_GRAD_RQ : (uint32_t)FMAX_GRAD;
       std::vector<uint32_t> rem;
       for (size_t k = i; k < j; ++k) rem.push_back((uint32_t)k);
       while (!rem.empty()) {
@@ -191,7 +253,7 @@ struct FusionPlanner {
               ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
           if ((backward && kind >= 0 && (int)meas != kind) || (q & blocked) ||
               (conflicts_of(cls) & left) || pass.size() >= fuse_max_ops ||
-              nred + isred > (uint32_t)FMAX_GRAD || !tile_fits(mask | op_bits(g), T)) {
+              nred + isred > gmax || !tile_fits(mask | op_bits(g), T)) {
             blocked |= q;
             left |= cls;
             rest.push_back(k);
@@ -207,6 +269,9 @@ struct FusionPlanner {
         } else {
           FusionItem it{2, pass};
           tile_config(mask, T, it.lc, it.h, it.hb);
+          bool gates_only = it.lc >= NLOW - LV;  // the low positions are tile bits
+          for (uint32_t k : pass) gates_only = gates_only && is_gate_op(plan[k]);
+          if (permute && gates_only) permute_after(it, plan, rest, j);
           items.push_back(it);
         }
         rem.swap(rest);
@@ -274,9 +339,27 @@ struct RqStage {
 };
 struct RqLayout {
   uint32_t slot[4];  // tile bit held by register slot s
+  // thread bits: the tile bits not in a slot, ascending — or, with tfix, tfirst[0..2] first
+  // (a permuting pass's store layout: the bits that land on chunk bits 0..2)
+  bool tfix = false;
+  uint32_t tfirst[3] = {0, 0, 0};
   bool operator==(const RqLayout& o) const {
     return slot[0] == o.slot[0] && slot[1] == o.slot[1] && slot[2] == o.slot[2] &&
-           slot[3] == o.slot[3];
+           slot[3] == o.slot[3] && tfix == o.tfix &&
+           (!tfix || (tfirst[0] == o.tfirst[0] && tfirst[1] == o.tfirst[1] &&
+                      tfirst[2] == o.tfirst[2]));
+  }
+  // the thread bits in order (k < T - 4)
+  uint32_t threads(uint32_t T, uint32_t* out) const {
+    uint32_t k = 0;
+    if (tfix)
+      for (int i = 0; i < 3; ++i) out[k++] = tfirst[i];
+    for (uint32_t q = 0; q < T && k < 8; ++q) {
+      if (holds(q)) continue;
+      if (tfix && (q == tfirst[0] || q == tfirst[1] || q == tfirst[2])) continue;
+      out[k++] = q;
+    }
+    return k;
   }
   int find(uint32_t q) const {
     for (int s = 0; s < 4; ++s)
@@ -312,23 +395,25 @@ inline rq_layout rq_descriptor(const RqLayout& L, uint32_t T) {
       if ((j >> s) & 1u) idx |= 1u << L.slot[s];
     d.rp[j] = swz(idx);
   }
-  uint32_t k = 0;
-  for (uint32_t q = 0; q < T && k < 8; ++q)
-    if (!L.holds(q)) d.tv[k++] = swz(1u << q);
+  uint32_t th[8];
+  const uint32_t nt = L.threads(T, th);
+  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = swz(1u << th[k]);
   return d;
 }
 // The HBM side of a load / store layout (rqio halves): chunk offsets of the thread bits and of
 // the register chunk index (slots 1..3), with tile chunk bit c at global chunk bit
 // c (c < lc) or hb[c - lc].
+// dest (store of a permuting pass): tile bit q's value goes where tile bit dest[q] sits.
 inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* hb,
-                   uint64_t* gv, uint64_t* offi) {
+                   uint64_t* gv, uint64_t* offi, const uint32_t* dest = nullptr) {
   auto gbit = [&](uint32_t tile_bit) -> uint64_t {  // tile bit >= 1 -> global chunk offset
-    const uint32_t c = tile_bit - 1;
+    const uint32_t c = (dest ? dest[tile_bit] : tile_bit) - 1;
     return 1ull << (c < lc ? c : hb[c - lc]);
   };
+  uint32_t th[8];
+  const uint32_t nt = L.threads(T, th);
   uint32_t k = 0;
-  for (uint32_t q = 0; q < T && k < 8; ++q)
-    if (!L.holds(q)) gv[k++] = gbit(q);
+  for (; k < nt; ++k) gv[k] = gbit(th[k]);
   for (; k < 8; ++k) gv[k] = 0;
   for (uint32_t i = 0; i < (uint32_t)RQ_R / 2; ++i) {
     uint64_t o = 0;
@@ -343,8 +428,11 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
 // register slots; when none does, relayout to the 4 qubits of the lowest ready stage plus
 // those of the stages that then become runnable, greedily in index order (a cover of the
 // coming stages), filled with the qubits of the next stages.  The pass starts in a load
-// layout chosen the same way under the HBM constraint, and ends in an HBM-valid layout.
-inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T) {
+// layout chosen the same way under the HBM constraint, and ends in an HBM-valid layout — for
+// a permuting pass (src != nullptr: src[b] = the tile bit whose value lands on tile bit b,
+// b < 4) the layout with slot 0 = src[0] and thread bits 0..2 = src[1..3].
+inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
+                      const uint32_t* src = nullptr) {
   const size_t n = st.size();
   auto qset = [&](size_t j, uint32_t* q) -> int {
     q[0] = st[j].t1;
@@ -451,7 +539,23 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T) {
     done |= 1ull << pick;
     --left;
   }
-  if (cur.hbm_ok()) {
+  if (src) {
+    RqLayout L{{src[0], ~0u, ~0u, ~0u}};
+    L.tfix = true;
+    for (int i = 0; i < 3; ++i) L.tfirst[i] = src[1 + i];
+    auto taken = [&](uint32_t q) {
+      for (int i = 0; i < 4; ++i)
+        if (src[i] == q) return true;
+      return L.holds(q);
+    };
+    for (int s = 1; s < 4; ++s)  // keep the current slots' qubits where possible
+      if (cur.slot[s] != ~0u && !taken(cur.slot[s])) L.slot[s] = cur.slot[s];
+    for (int s = 1; s < 4; ++s)
+      for (uint32_t q = T; L.slot[s] == ~0u && q-- > 0;)
+        if (!taken(q)) L.slot[s] = q;
+    P.store = L;
+    P.steps.push_back(RqStep{true, P.store, 0, 0});
+  } else if (cur.hbm_ok()) {
     P.store = cur;
   } else {
     std::vector<uint32_t> S{0u};

@@ -551,6 +551,13 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
 // ---------------------------------------------------------------------------------------
 constexpr int FMAX_OPS = 32;   // gates per fused pass (>= its stages)
 constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (>= its gradient stages)
+#ifndef QDC_FMAX_GRAD_RQ
+#define QDC_FMAX_GRAD_RQ 16
+#endif
+// the same for register-resident two-state passes (per-wave LDS accumulators).  Measured at
+// C2 n=28: 24 / 32 give 20 % / 15 % fewer reverse passes, each 33 % / 23 % slower (more
+// relayouts per stage, 7 / 6 blocks per CU): 16 is best.
+constexpr int FMAX_GRAD_RQ = QDC_FMAX_GRAD_RQ;
 constexpr int FMAX_ROWS = 8;   // far qubits per tile
 constexpr int FACC = 32;       // reals per gradient accumulator (16 complex)
 
@@ -705,7 +712,8 @@ __device__ __forceinline__ void half_swap(double& a, double& b) {
 // pair; offsets 8, 4, 2, 1 are DPP moves (row_ror:8, row_half_mirror, quad_perm) with lane
 // selects.  Partner lanes always agree on the bits above the current offset, so they hold the
 // same index set; the lane with the offset bit set keeps the upper half.
-template <int V>
+// ATOMIC: several waves add into the same LDS accumulators (ds_add_f32)
+template <int V, bool ATOMIC = false>
 __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
   constexpr uint64_t UPPER[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull,
                                  0xFF00FF00FF00FF00ull, 0xF0F0F0F0F0F0F0F0ull,
@@ -759,7 +767,12 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
     }
   }
   const int spread = 64 / V;  // lanes holding the same idx
-  if ((lane & (spread - 1)) == 0) acc[idx] += x[0];
+  if ((lane & (spread - 1)) == 0) {
+    if constexpr (ATOMIC)
+      atomicAdd(&acc[idx], x[0]);
+    else
+      acc[idx] += x[0];
+  }
 }
 
 // LDS layout of a fused tile: XOR-swizzled so that lanes of one LDS access spread over all

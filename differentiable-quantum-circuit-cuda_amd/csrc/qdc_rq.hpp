@@ -252,11 +252,11 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   constexpr int CPT = RQ_R / VEC;  // chunks of each state per thread (8)
   constexpr int TA = NT * RQ_R;    // amplitudes per tile and state
   __shared__ cx buf[TA];
-  __shared__ real accw[TWO ? NT / 64 : 1][TWO ? FMAX_GRAD : 1][FACC];
+  __shared__ real accw[TWO ? NT / 64 : 1][TWO ? FMAX_GRAD_RQ : 1][FACC];
   const uint32_t t = threadIdx.x;
   const int wave = (int)(t >> 6);
   if constexpr (TWO) {
-    for (uint32_t i = t; i < (NT / 64) * FMAX_GRAD * FACC; i += NT) (&accw[0][0][0])[i] = 0;
+    for (uint32_t i = t; i < (NT / 64) * FMAX_GRAD_RQ * FACC; i += NT) (&accw[0][0][0])[i] = 0;
     // a wave's accumulators are zeroed partly by other waves; a Gamma stage can come before
     // the pass's first relayout barrier
     __syncthreads();
@@ -333,7 +333,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       const uint32_t kind = op.kind & 7u;
       const bool gamma = TWO && (op.kind & FOP_GAMMA);
       const cx* M = mats + op.mat;
-      real* acc = TWO ? &accw[wave][ri < FMAX_GRAD ? ri : 0][0] : nullptr;
+      real* acc = TWO ? &accw[wave][ri < FMAX_GRAD_RQ ? ri : 0][0] : nullptr;
       if (kind == FK_RELAYOUT) {
         const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
         const uint32_t tpn = rq_tp<LOGNT>(Ln, t);

@@ -54,6 +54,14 @@ struct QubitMap {
     for (uint32_t q = 0; q < n; ++q) phys[q] = np[phys[q]];
     for (uint32_t q = 0; q < n; ++q) logi[phys[q]] = q;
   }
+  // exchange the qubits at physical positions a and b (a permuting fused pass's store)
+  void swap_phys(uint32_t a, uint32_t b) {
+    const uint32_t la = logi[a], lb = logi[b];
+    phys[la] = b;
+    phys[lb] = a;
+    logi[a] = lb;
+    logi[b] = la;
+  }
 };
 
 inline bool instr_is_q1(int kind) {

@@ -68,7 +68,7 @@ def qubits(ins, op):
     return set(p)
 
 
-def check_invariants(n, ins, sens, mode, prec, ops, items):
+def check_invariants(n, ins, sens, mode, prec, ops, items, permuted=False):
     backward = mode == 2
     order = [i for it in items for st in it["stages"] for i in st]
     assert sorted(order) == list(range(len(ops)))
@@ -100,8 +100,8 @@ def check_invariants(n, ins, sens, mode, prec, ops, items):
         assert it["lc"] >= 3 and it["lc"] + it["h"] == tbits
         tile = set(range(LV[prec] + it["lc"])) | {LV[prec] + c for c in it["hb"]}
         members = [i for st in it["stages"] for i in st]
-        for i in members:
-            assert qubits(ins, ops[i]) <= tile | set(range(LV[prec])), (i, it)
+        for i in members:  # (permuting passes move qubits: tiles are in the permuted layout)
+            assert permuted or qubits(ins, ops[i]) <= tile | set(range(LV[prec])), (i, it)
         if backward:
             assert len({meas[i] for i in members}) == 1
             assert len({i >= first_inject for i in members}) == 1
@@ -180,8 +180,23 @@ def replay(n, ins, ops, items, gates, psi0, cot_fn):
     return dlist, [grads[i] for i in sorted(grads)], state
 
 
+@pytest.mark.parametrize("n,seed", [(14, 1), (24, 3)])
+def test_permuting_schedule_invariants(monkeypatch, n, seed):
+    """The f32 runtime's register-resident settings (QDC_SCHED_RQ: gate-only passes permute
+    their tile's qubits, later positions are rewritten): ordering invariants still hold."""
+    monkeypatch.setenv("QDC_SCHED_RQ", "1")
+    ins, const, var, gates, sens = make(n, seed)
+    for mode in (0, 1, 2):
+        ops, items = schedule(n, ins, mode, sens, "f32")
+        check_invariants(n, ins, sens, mode, "f32", ops, items, permuted=True)
+
+
+@pytest.mark.parametrize("sched_rq", ["0", "1"])
 @pytest.mark.parametrize("perturb", [0.0, 1e-3])
-def test_schedule_replay_matches_sequential_oracle(perturb):
+def test_schedule_replay_matches_sequential_oracle(monkeypatch, perturb, sched_rq):
+    """Replaying the scheduled execution order (logical qubits) equals the sequential oracle;
+    sched_rq = 1 uses the runtime's f32 permuting planner."""
+    monkeypatch.setenv("QDC_SCHED_RQ", sched_rq)
     n = 12  # the smallest n whose tiles are full in both passes (f32: 2^11 chunks)
     ins, const, var, gates, sens = make(n, 11, perturb)
     ops, items = {}, {}

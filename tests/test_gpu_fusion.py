@@ -237,3 +237,34 @@ def test_register_resident_passes_equal_lds_passes(case):
         assert normrel(res[rq][0], want_d) < TOL["f32"], rq
         assert normrel(res[rq][1], want_g) < TOL["f32"] * 10, rq
     assert normrel(res[1][1], res[0][1]) < TOL["f32"]
+
+
+@pytest.mark.parametrize("n", [13, 18])
+def test_permuting_passes_equal_fixed_layout(n):
+    """f32 gate-only passes permute their tile's qubits on the way out (QDC_RQ_PERM=1, the
+    default; later ops run at rewritten positions).  Densities, gradients and the forward and
+    uncomputed states (read back in logical order) equal the fixed-layout run and the oracle."""
+    dt = np.complex64
+    ins, var = O.layered_circuit(n, 5, seed=n)
+    vg = [g.astype(dt) for g in var]
+    res = {}
+    for perm in (0, 1):
+        c = build_env("f32", n, ins, {"QDC_RQ_PERM": perm, "QDC_FUSE": 1})
+        d = c.forward([], vg)
+        fwd_state = c.get_state(0)
+        phys = c.layout()[0]
+        g = c.backward([np.diag([1.0, -1.0]).astype(dt) for _ in d], [], vg)
+        res[perm] = (d, g, fwd_state, c.get_state(0), list(phys))
+    assert res[1][4] != list(range(n))  # the permuting run did leave a permuted layout
+    o = O.OracleCircuit(n, dt)
+    for k, pos in ins:
+        o.add(k, *pos)
+    want_d = o.forward([], vg)
+    want_state = o.state.copy()
+    want_g = o.backward([np.diag([1.0, -1.0]).astype(dt) for _ in want_d], [], vg)
+    for perm in (0, 1):
+        d, g, fs, us, _ = res[perm]
+        assert normrel(d, want_d) < TOL["f32"]
+        assert normrel(g, want_g) < TOL["f32"] * 10
+        assert normrel([fs], [want_state]) < TOL["f32"]
+        assert abs(us[0] - 1) < 1e-4 and np.abs(us[1:]).max() < 1e-4
