@@ -94,7 +94,31 @@ QDC_API const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex
   qdc::Circuit& k = c->impl;
   if (k.g != 0) return qdc::fail("sharded state: use qdc_circuit_get_shard and qdc_circuit_layout");
   if (len != ((size_t)1 << k.n)) return qdc::fail("state length mismatch");
-  return qdc_circuit_get_shard(c, which, 0, host, len);
+  QDC_TRY(qdc_circuit_get_shard(c, which, 0, host, len));
+  // fused passes may leave fwd / bwd in a permuted qubit layout; `initial` never is
+  bool ident = true;
+  for (uint32_t q = 0; q < k.n; ++q) ident = ident && k.layout.phys[q] == q;
+  if (which == 1 || ident) return nullptr;
+  std::vector<qdc_complex> phys(host, host + len);
+  // logical index i -> physical index: OR of per-11-bit-field tables
+  constexpr uint32_t FB = 11;
+  const uint32_t nf = (k.n + FB - 1) / FB;
+  std::vector<std::vector<size_t>> tab(nf);
+  for (uint32_t f = 0; f < nf; ++f) {
+    const uint32_t lo = f * FB, w = std::min(FB, k.n - lo);
+    tab[f].resize((size_t)1 << w);
+    for (size_t v = 0; v < tab[f].size(); ++v) {
+      size_t p = 0;
+      for (uint32_t b = 0; b < w; ++b) p |= ((v >> b) & 1u) << k.layout.phys[lo + b];
+      tab[f][v] = p;
+    }
+  }
+  for (size_t i = 0; i < len; ++i) {
+    size_t p = 0;
+    for (uint32_t f = 0; f < nf; ++f) p |= tab[f][(i >> (f * FB)) & (tab[f].size() - 1)];
+    host[i] = phys[p];
+  }
+  return nullptr;
 }
 
 QDC_API const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world,

@@ -203,10 +203,8 @@ class _CircuitBase:
         phys, world, rank0, nlocal = self.layout()
         if world == 1:
             out = np.empty(1 << self._n, dtype=self._dtype)
+            # (logical order: the library undoes a permuted single-device layout)
             check(self._lib.qdc_circuit_get_state(self._h, which, ptr(out), out.size))
-            # fused passes may leave fwd/bwd in a permuted qubit layout; `initial` never is
-            if which != 1 and list(phys) != list(range(self._n)):
-                out = unpermute(out, phys)
             return out
         shards = [self.get_shard(which, s) for s in range(nlocal)]
         if nlocal < world:

@@ -89,7 +89,8 @@ const char* qdc_circuit_backward(qdc_circuit* c, const qdc_complex* dens_grads,
 
 /* Copies of the device states, for tests and debugging (QuantizedTensor::get_cpu_state_copy,
  * quantized_tensor.rs:91-99).  which: 0 = current (fwd) state, 1 = initial state,
- * 2 = backward state (after a backward call). */
+ * 2 = backward state (after a backward call).  Always in logical qubit order (fused passes
+ * may keep fwd / bwd in a permuted layout on the device: qdc_circuit_layout). */
 const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex* host, size_t len);
 
 /* Wait for all work queued by this circuit. */
