@@ -221,6 +221,26 @@ def dense_gate_sample(args, n):
     return out
 
 
+def vqse_sample(steps=3):
+    """Config C3 (example_vqse_ising.py at its own size: n = 26, 26 layers, f64, |+>^n): wall
+    seconds per loss-and-gradient call, the number the example prints (example:133)."""
+    sys.path.insert(0, str(ROOT / "examples"))
+    import vqse_ising
+    from quantum_differentiable_circuit import workloads as W
+    n, layers = 26, 26
+    f = vqse_ising.build(n, layers, "f64")
+    h = W.tfim_term(1.0)
+    p = np.random.default_rng(42).normal(size=2 * layers)
+    W.vqse_loss_and_grad(f, p, n, h)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e, _ = W.vqse_loss_and_grad(f, p, n, h)
+    dt = (time.perf_counter() - t0) / steps
+    return {"s_per_loss_grad_call": round(dt, 4), "energy": round(e, 6), "qubits": n,
+            "layers": layers, "gates": 2 * n * layers, "dtype": "c128 (f64)",
+            "calls": steps}
+
+
 def micro(args):
     """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse
     (single-gate kernels: fusion off)."""
@@ -361,10 +381,11 @@ def main():
     eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / max(world, 1)
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
-    gate_kernels = dense_kernels = None
+    gate_kernels = dense_kernels = vqse = None
     if rank == 0 and world == 1 and not args.no_gate_sample:
         gate_kernels = gate_kernel_sample(args, n)
         dense_kernels = dense_gate_sample(args, n)
+        vqse = vqse_sample()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -410,6 +431,7 @@ def main():
             "effective_gate_bandwidth": effective,
             "gate_kernels": gate_kernels,
             "dense_gate_kernels": dense_kernels,
+            "vqse_c3": vqse,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
