@@ -383,13 +383,22 @@ def main():
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
     gate_kernels = dense_kernels = vqse = None
     if rank == 0 and world == 1 and not args.no_gate_sample:
-        gate_kernels = gate_kernel_sample(args, n)
-        dense_kernels = dense_gate_sample(args, n)
-        vqse = vqse_sample()
+        # auxiliary samples: a failure there is reported in the line, never loses the headline
+        def aux(fn, *a):
+            try:
+                return fn(*a)
+            except Exception as e:  # noqa: BLE001
+                return {"error": f"{type(e).__name__}: {e}"[:300]}
+        gate_kernels = aux(gate_kernel_sample, args, n)
+        dense_kernels = aux(dense_gate_sample, args, n)
+        vqse = aux(vqse_sample)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.cpu_qubits or n)
+        try:
+            cpu = cpu_baseline(args, args.cpu_qubits or n)
+        except Exception as e:  # noqa: BLE001
+            cpu = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     if rank == 0:
         state_gib = (1 << n) * (8 if args.precision == "f32" else 16) / 2**30
