@@ -720,7 +720,10 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
                                  0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};
   constexpr int CTRL[6] = {0, 0, 0x128 /*row_ror:8*/, 0x141 /*row_half_mirror*/,
                            0x4E /*quad_perm 2,3,0,1*/, 0xB1 /*quad_perm 1,0,3,2*/};
-  const int lane = threadIdx.x & 63;
+  // opaque lane: keeps the compiler from hoisting this call's lane-derived index out of the
+  // pass loop (a long-lived VGPR that spilled and was reloaded, with a vmcnt wait, per stage)
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   int idx = 0;
 #pragma unroll
   for (int step = 0; step < 6; ++step) {

@@ -254,7 +254,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   __shared__ cx buf[TA];
   __shared__ real accw[TWO ? NT / 64 : 1][TWO ? FMAX_GRAD_RQ : 1][FACC];
   const uint32_t t = threadIdx.x;
-  const int wave = (int)(t >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(t >> 6));
   if constexpr (TWO) {
     for (uint32_t i = t; i < (NT / 64) * FMAX_GRAD_RQ * FACC; i += NT) (&accw[0][0][0])[i] = 0;
     // a wave's accumulators are zeroed partly by other waves; a Gamma stage can come before
@@ -271,7 +271,6 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       thr_st += io->gv_st[k];
     }
   }
-  const uint32_t tp0 = rq_tp<LOGNT>(L0, t);
   const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
   const uint32_t count =
       tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
@@ -325,8 +324,9 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     }
   };
   auto run = [&](cx (&xf)[RQ_R], cx (&xb)[RQ_R]) __attribute__((always_inline)) {
-    uint32_t tp = tp0;
-    const rq_layout* Lc = L0;
+    // loop state kept small (register pressure): the current layout as a uniform offset into
+    // the program; the per-thread LDS parts are recomputed at each relayout
+    uint32_t lcur = l0;
     uint32_t ri = 0;
     for (uint32_t j = 0; j < fg.nops; ++j) {
       const fop op = ops[j];
@@ -335,12 +335,12 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       const cx* M = mats + op.mat;
       real* acc = TWO ? &accw[wave][ri < FMAX_GRAD_RQ ? ri : 0][0] : nullptr;
       if (kind == FK_RELAYOUT) {
+        const rq_layout* Lc = reinterpret_cast<const rq_layout*>(mats + lcur);
         const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
-        const uint32_t tpn = rq_tp<LOGNT>(Ln, t);
+        const uint32_t tp = rq_tp<LOGNT>(Lc, t), tpn = rq_tp<LOGNT>(Ln, t);
         rq_exchange(xf, buf, tp, Lc, tpn, Ln);
         if constexpr (TWO) rq_exchange(xb, buf, tp, Lc, tpn, Ln);
-        tp = tpn;
-        Lc = Ln;
+        lcur = op.mat;
         continue;
       }
       // slot case (host: rq_plan): two-qubit / diagonal S1 * 4 + S2 (t1 in slot S1, t2 in
