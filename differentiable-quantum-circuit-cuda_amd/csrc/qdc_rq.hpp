@@ -327,6 +327,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     // loop state kept small (register pressure): the current layout as a uniform offset into
     // the program; the per-thread LDS parts are recomputed at each relayout
     uint32_t lcur = l0;
+    uint32_t tpc = TWO ? 0u : rq_tp<LOGNT>(reinterpret_cast<const rq_layout*>(mats + l0), t);
     uint32_t ri = 0;
     for (uint32_t j = 0; j < fg.nops; ++j) {
       const fop op = ops[j];
@@ -337,9 +338,11 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       if (kind == FK_RELAYOUT) {
         const rq_layout* Lc = reinterpret_cast<const rq_layout*>(mats + lcur);
         const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
-        const uint32_t tp = rq_tp<LOGNT>(Lc, t), tpn = rq_tp<LOGNT>(Ln, t);
+        // two-state: recomputed (register pressure); one-state: carried
+        const uint32_t tp = TWO ? rq_tp<LOGNT>(Lc, t) : tpc, tpn = rq_tp<LOGNT>(Ln, t);
         rq_exchange(xf, buf, tp, Lc, tpn, Ln);
         if constexpr (TWO) rq_exchange(xb, buf, tp, Lc, tpn, Ln);
+        tpc = tpn;
         lcur = op.mat;
         continue;
       }
