@@ -298,7 +298,8 @@ QDC_API size_t qdc_rq_plan(unsigned tile_bits, const unsigned* kinds, const unsi
                            unsigned* steps, size_t cap) {
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
-  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits);
+  const char* mc = getenv("QDC_RQ_MAXCL");  // the runtime's knob (qdc_circuit.hpp)
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, !(mc && atoi(mc) == 0));
   if (plan.steps.size() + 2 > cap) return SIZE_MAX;
   auto put = [&](size_t i, unsigned kind, unsigned stage, unsigned cs, const qdc::RqLayout& L) {
     unsigned* o = steps + 7 * i;

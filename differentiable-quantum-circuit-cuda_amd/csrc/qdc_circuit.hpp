@@ -151,6 +151,7 @@ struct Circuit {
   int rq_prefetch = 1;      // register-resident passes prefetch the next tile (QDC_RQ_PF)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
+  int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -185,6 +186,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PF")) rq_prefetch = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
+    if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -693,7 +695,7 @@ struct Circuit {
           if (dest[t] < 4) src[dest[t]] = t;
         }
       }
-      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr);
+      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0);
       it.l0 = put_layout(P.load);
       {  // rqio after the load descriptor
         rqio io{};
@@ -918,7 +920,11 @@ struct Circuit {
     std::vector<qdc_plan_op> pl = plan(mode);
     std::vector<Item> items = fuse_items(pl, false);
     size_t mats_off = 0;
+    const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
+    if (rq_stats)
+      fprintf(stderr, "forward plan+build %.3f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     for (const Item& item : items) {
       if (item.type == 2) {
         QDC_TRY(run_fused(item, false, mats_off, false));
@@ -1007,8 +1013,12 @@ struct Circuit {
       }
     std::vector<Item> items = fuse_items(pl, true, first_inject);
     size_t mats_off = 0;
+    const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
                           (uint32_t)nvar, {}, &dg));
+    if (rq_stats)
+      fprintf(stderr, "backward plan+build %.3f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     for (const Item& item : items) {
       if (item.type == 2) {
         const bool two = item.ops[0] >= first_inject;

@@ -425,14 +425,18 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
 
 // Schedule a pass's stages on register layouts (T tile bits).  List scheduling: among the
 // stages whose dependencies are done, run (lowest index first) one whose qubits sit in
-// register slots; when none does, relayout to the 4 qubits of the lowest ready stage plus
-// those of the stages that then become runnable, greedily in index order (a cover of the
-// coming stages), filled with the qubits of the next stages.  The pass starts in a load
+// register slots; when none does, relayout.  A relayout's qubit set is a cover: the 4 qubits
+// of a ready seed stage plus those of the stages that then become runnable, greedily in index
+// order, filled with the qubits of the next stages.  Every ready stage is tried as the seed and
+// the cover that runs the most stages before the next relayout wins (max closure; with
+// max_closure = false, the lowest ready seed).  A last relayout whose cover runs every
+// remaining stage is made an HBM layout if it can be, which saves the store's relayout
+// (C2 n=28: 507 -> 497 relayouts per step, +1 % gates/s; random passes -8..16 %).  The pass starts in a load
 // layout chosen the same way under the HBM constraint, and ends in an HBM-valid layout — for
 // a permuting pass (src != nullptr: src[b] = the tile bit whose value lands on tile bit b,
 // b < 4) the layout with slot 0 = src[0] and thread bits 0..2 = src[1..3].
 inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
-                      const uint32_t* src = nullptr) {
+                      const uint32_t* src = nullptr, bool max_closure = true) {
   const size_t n = st.size();
   auto qset = [&](size_t j, uint32_t* q) -> int {
     q[0] = st[j].t1;
@@ -502,35 +506,72 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
     }
     return L;
   };
+  // stages that run on the qubit set S from `done` on, without another relayout
+  auto closure = [&](uint64_t done0, const std::vector<uint32_t>& S) {
+    uint32_t smask = 0;
+    for (uint32_t q : S) smask |= 1u << q;
+    uint64_t sim = done0;
+    int cnt = 0;
+    for (bool progress = true; progress;) {
+      progress = false;
+      for (size_t c = 0; c < n; ++c) {
+        if (((sim >> c) & 1ull) || (st[c].deps & ~sim) != 0) continue;
+        if (!((smask >> st[c].t1) & 1u) || !((smask >> st[c].t2) & 1u)) continue;
+        sim |= 1ull << c;
+        ++cnt;
+        progress = true;
+      }
+    }
+    return cnt;
+  };
+  auto ready = [&](uint64_t done0, size_t j) {
+    return !((done0 >> j) & 1ull) && (st[j].deps & ~done0) == 0;
+  };
+  // Max closure: every ready stage seeds a cover; the one that runs the most stages before
+  // the next relayout wins (ties: the lowest seed).  With `hbm` (the load layout, or a last
+  // layout that is also the store) the seeds are the stages an HBM layout can hold.
+  auto best_cover = [&](uint64_t done0, const std::vector<uint32_t>& base, bool hbm) {
+    std::vector<uint32_t> best;
+    int best_cnt = -1;
+    for (size_t j = 0; j < n; ++j) {
+      if (!ready(done0, j)) continue;
+      if (hbm && !(hbm_allowed(st[j].t1) && hbm_allowed(st[j].t2))) continue;
+      std::vector<uint32_t> S = cover(done0, j, base, hbm);
+      if (!max_closure) return S;  // greedy: the lowest ready seed
+      const int cnt = closure(done0, S);
+      if (cnt > best_cnt) {
+        best_cnt = cnt;
+        best = std::move(S);
+      }
+    }
+    if (best_cnt < 0) best = cover(done0, n, base, hbm);
+    return best;
+  };
   RqPlan P;
   uint64_t done = 0;
   {  // load layout
-    size_t j0 = n;
-    for (size_t j = 0; j < n && j0 == n; ++j) {
-      uint32_t q[2];
-      const int m = qset(j, q);
-      bool ok = st[j].deps == 0;
-      for (int i = 0; i < m; ++i) ok = ok && hbm_allowed(q[i]);
-      if (ok) j0 = j;
-    }
     const RqLayout none{{~0u, ~0u, ~0u, ~0u}};
-    P.load = place(cover(0, j0, {0u}, true), none, true);
+    P.load = place(best_cover(0, {0u}, true), none, true);
   }
   RqLayout cur = P.load;
   for (size_t left = n; left > 0;) {
-    size_t pick = n, first_ready = n;
-    for (size_t j = 0; j < n; ++j) {
-      if (((done >> j) & 1ull) || (st[j].deps & ~done) != 0) continue;
-      if (first_ready == n) first_ready = j;
-      if (fits(cur, j)) {
-        pick = j;
-        break;
-      }
-    }
+    size_t pick = n;
+    for (size_t j = 0; j < n && pick == n; ++j)
+      if (ready(done, j) && fits(cur, j)) pick = j;
     if (pick == n) {
-      cur = place(cover(done, first_ready, {}, false), cur, false);
+      // a cover that runs every remaining stage and is itself an HBM layout saves the
+      // relayout back at the end (plain passes: a permuting pass stores through src)
+      std::vector<uint32_t> S;
+      bool hbm = false;
+      if (!src && max_closure) {
+        S = best_cover(done, {0u}, true);
+        hbm = closure(done, S) == (int)left;
+      }
+      if (!hbm) S = best_cover(done, {}, false);
+      cur = place(S, cur, hbm);
       P.steps.push_back(RqStep{true, cur, 0, 0});
-      pick = first_ready;
+      for (size_t j = 0; j < n && pick == n; ++j)
+        if (ready(done, j) && fits(cur, j)) pick = j;
     }
     const RqStage& s = st[pick];
     const uint32_t cs = s.kind == FK_Q1 ? (uint32_t)cur.find(s.t1)
