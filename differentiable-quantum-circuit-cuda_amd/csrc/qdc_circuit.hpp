@@ -152,6 +152,7 @@ struct Circuit {
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
+  uint32_t rq_perm_low = 0;  // low positions a permuting pass fills, 0: default (QDC_RQ_PERM_LOW)
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -187,6 +188,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
+    if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -396,6 +398,7 @@ struct Circuit {
     // (single-device layout only: the sharded remap planner owns the layout there)
     P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
     P.rq_grad = rq_grad32 && use_rq && sizeof(real) == 4;
+    if (rq_perm_low) P.perm_low = rq_perm_low;
     return P;
   }
   bool is_meas(const qdc_plan_op& op) const { return planner().is_meas(op); }

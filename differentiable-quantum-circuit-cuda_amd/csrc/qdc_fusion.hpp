@@ -81,6 +81,9 @@ struct FusionPlanner {
   bool permute = false;
   // two-state gate passes run register-resident (k_rq: FMAX_GRAD_RQ Gamma accumulators)
   bool rq_grad = false;
+  // low physical positions a permuting pass fills with the qubits the next ops need first
+  // (>= NLOW; more makes the next tiles' contiguous runs longer)
+  uint32_t perm_low = (uint32_t)LV + 3;
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -160,6 +163,8 @@ struct FusionPlanner {
   // segment, then plan[next..]) that uses them; the first NLOW move to the low positions.
   void permute_after(FusionItem& it, std::vector<qdc_plan_op>& plan,
                      const std::vector<uint32_t>& rest, size_t next) const {
+    // the low positions to fill: at least NLOW, at most the pass's contiguous run
+    const uint32_t nlow = std::max(NLOW, std::min(perm_low, (uint32_t)LV + it.lc));
     std::vector<uint8_t> in_tile(nl, 0);
     for (uint32_t p = 0; p < (uint32_t)LV + it.lc; ++p) in_tile[p] = 1;
     for (uint32_t r = 0; r < it.h; ++r) in_tile[LV + it.hb[r]] = 1;
@@ -168,22 +173,22 @@ struct FusionPlanner {
     auto see = [&](const qdc_plan_op& op) {
       if (op.type != QDC_PLAN_OP) return;
       for (uint32_t p : {op.pos2, op.pos1})
-        if (p < nl && in_tile[p] && !ranked[p] && want.size() < NLOW) {
+        if (p < nl && in_tile[p] && !ranked[p] && want.size() < nlow) {
           ranked[p] = 1;
           want.push_back(p);
         }
     };
     for (uint32_t k : rest) see(plan[k]);
-    for (size_t k = next; k < plan.size() && want.size() < NLOW; ++k) {
+    for (size_t k = next; k < plan.size() && want.size() < nlow; ++k) {
       if (plan[k].type == QDC_PLAN_REMAP) break;
       see(plan[k]);
     }
     std::vector<uint32_t> free_low;  // low positions whose qubit is not wanted
-    for (uint32_t p = 0; p < NLOW; ++p)
+    for (uint32_t p = 0; p < nlow; ++p)
       if (!ranked[p]) free_low.push_back(p);
     size_t f = 0;
     for (uint32_t p : want)
-      if (p >= NLOW) it.swaps.push_back({p, free_low[f++]});
+      if (p >= nlow) it.swaps.push_back({p, free_low[f++]});
     if (it.swaps.empty()) return;
     auto moved = [&](uint32_t p) {
       for (const auto& sw : it.swaps) {
