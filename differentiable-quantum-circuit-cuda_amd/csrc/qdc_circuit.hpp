@@ -148,7 +148,8 @@ struct Circuit {
   int fuse_meas = 1;        // densities / cotangent injections join fused passes
   int use_rq = 1;           // f32 gate passes run register-resident (qdc_rq.hpp)
   int rq_stats = 0;
-  int rq_prefetch = 1;      // register-resident passes prefetch the next tile (QDC_RQ_PF)
+  int rq_prefetch = 1;      // one-state register-resident passes prefetch the next tile (QDC_RQ_PF)
+  int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
@@ -185,6 +186,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ")) use_rq = atoi(e);
     if (const char* e = getenv("QDC_RQ_STATS")) rq_stats = atoi(e);
     if (const char* e = getenv("QDC_RQ_PF")) rq_prefetch = atoi(e);
+    if (const char* e = getenv("QDC_RQ_PF2")) rq_prefetch2 = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
@@ -764,10 +766,9 @@ struct Circuit {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     const void* kern = nullptr;
-    // the next tile's prefetch pays in one-state passes only: two-state ones would double 64
-    // state VGPRs and drop to 2 waves/SIMD (measured 4 % slower at C2 n=28)
-    const bool pf = rq_prefetch != 0 && !two;
-    if (two && nt == 128) kern = (const void*)k_rq<true, 128, false>;
+    // the next tile's loads are in flight while this tile's stages run (2 waves/SIMD)
+    const bool pf = two ? rq_prefetch2 != 0 : rq_prefetch != 0;
+    if (two && nt == 128) kern = pf ? (const void*)k_rq<true, 128, true> : (const void*)k_rq<true, 128, false>;
     else if (!two && nt == 128) kern = pf ? (const void*)k_rq<false, 128, true> : (const void*)k_rq<false, 128, false>;
     else if (!two && nt == 256) kern = pf ? (const void*)k_rq<false, 256, true> : (const void*)k_rq<false, 256, false>;
     else return fail("no register-resident kernel for a %u-amplitude %s tile", 1u << tbits,
@@ -786,6 +787,7 @@ struct Circuit {
     return ctx.launch_block(name, bytes, k_rq<T, N, P>, grid, nt, f, b, fops, mats, g, l0, \
                             partials, stride);
     QDC_RQ_LAUNCH(true, 128, false)
+    QDC_RQ_LAUNCH(true, 128, true)
     QDC_RQ_LAUNCH(false, 128, true)
     QDC_RQ_LAUNCH(false, 128, false)
     QDC_RQ_LAUNCH(false, 256, true)

@@ -713,8 +713,23 @@ __device__ __forceinline__ void half_swap(double& a, double& b) {
 // selects.  Partner lanes always agree on the bits above the current offset, so they hold the
 // same index set; the lane with the offset bit set keeps the upper half.
 // ATOMIC: several waves add into the same LDS accumulators (ds_add_f32)
+// Timing-only ablation builds (tools/ablate.sh; results are wrong): QDC_RQ_ABL bit 0 no stage
+// math, bit 1 no relayouts, bit 2 no Gamma, bit 3 Gamma without the wave reduction, bit 4
+// relayouts without barriers (qdc_rq.hpp).
+#ifndef QDC_RQ_ABL
+#define QDC_RQ_ABL 0
+#endif
 template <int V, bool ATOMIC = false>
 __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
+#if QDC_RQ_ABL & 8
+  {
+    real s = 0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += x[i];
+    acc[threadIdx.x & (V - 1)] += s;
+    return;
+  }
+#endif
   constexpr uint64_t UPPER[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull,
                                  0xFF00FF00FF00FF00ull, 0xF0F0F0F0F0F0F0F0ull,
                                  0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};

@@ -227,12 +227,87 @@ __device__ __forceinline__ uint32_t rq_tp(const rq_layout* L, uint32_t t) {
 __device__ __forceinline__ void rq_exchange(cx (&x)[RQ_R], cx* buf, uint32_t tp,
                                             const rq_layout* Lc, uint32_t tpn,
                                             const rq_layout* Ln) {
+#if !(QDC_RQ_ABL & 16)
   __syncthreads();  // every thread is done reading the buffer's previous contents
+#endif
 #pragma unroll
   for (int j = 0; j < RQ_R; ++j) buf[tp ^ Lc->rp[j]] = x[j];
+#if !(QDC_RQ_ABL & 16)
   __syncthreads();
+#endif
 #pragma unroll
   for (int j = 0; j < RQ_R; ++j) x[j] = buf[tpn ^ Ln->rp[j]];
+}
+
+// Prefetch loads the compiler's waitcnt pass does not see.  With ordinary loads it drains the
+// whole prefetch (s_waitcnt vmcnt(0)) at the first stage of the pass loop: a loop that reads
+// registers loaded outside it gets its vector-memory counter flushed, so the next tile's
+// loads never overlapped this tile's stages.  These loads are waited for explicitly (counted:
+// the wave's younger vector-memory ops are known at every wait).  Their destinations are fixed
+// physical VGPRs, the same in the load and in the wait (a tied in/out operand of the wait
+// asm), so the register allocator never has a reason to copy an in-flight register: a copy
+// before the wait would read stale data.  tools/check_rq_isa.py checks the ISA for any read
+// of them between a load and its wait.
+// Pinned registers: one-state passes v[96:127] (8 chunks), two-state v[192:255] (16 chunks).
+constexpr int RQ_PIN_ONE = 96, RQ_PIN_TWO = 192;
+template <int REG>
+__device__ __forceinline__ vec16 rq_ld(const chunk* p) {
+  vec16 v;
+  switch (REG) {
+    case 96: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[96:99]}"(v) : "v"(p) : "memory"); break;
+    case 100: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[100:103]}"(v) : "v"(p) : "memory"); break;
+    case 104: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[104:107]}"(v) : "v"(p) : "memory"); break;
+    case 108: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[108:111]}"(v) : "v"(p) : "memory"); break;
+    case 112: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[112:115]}"(v) : "v"(p) : "memory"); break;
+    case 116: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[116:119]}"(v) : "v"(p) : "memory"); break;
+    case 120: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[120:123]}"(v) : "v"(p) : "memory"); break;
+    case 124: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[124:127]}"(v) : "v"(p) : "memory"); break;
+    case 192: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[192:195]}"(v) : "v"(p) : "memory"); break;
+    case 196: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[196:199]}"(v) : "v"(p) : "memory"); break;
+    case 200: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[200:203]}"(v) : "v"(p) : "memory"); break;
+    case 204: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[204:207]}"(v) : "v"(p) : "memory"); break;
+    case 208: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[208:211]}"(v) : "v"(p) : "memory"); break;
+    case 212: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[212:215]}"(v) : "v"(p) : "memory"); break;
+    case 216: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[216:219]}"(v) : "v"(p) : "memory"); break;
+    case 220: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[220:223]}"(v) : "v"(p) : "memory"); break;
+    case 224: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[224:227]}"(v) : "v"(p) : "memory"); break;
+    case 228: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[228:231]}"(v) : "v"(p) : "memory"); break;
+    case 232: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[232:235]}"(v) : "v"(p) : "memory"); break;
+    case 236: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[236:239]}"(v) : "v"(p) : "memory"); break;
+    case 240: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[240:243]}"(v) : "v"(p) : "memory"); break;
+    case 244: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[244:247]}"(v) : "v"(p) : "memory"); break;
+    case 248: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[248:251]}"(v) : "v"(p) : "memory"); break;
+    case 252: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={v[252:255]}"(v) : "v"(p) : "memory"); break;
+  }
+  return v;
+}
+// vmcnt(0) on a wave's first tile (nothing issued after its loads), else vmcnt(N)
+#define QDC_RQ_WAIT_ASM                                     \
+  "s_cmp_eq_u32 %[first], 0\n\t"                           \
+  "s_cbranch_scc1 1f\n\t"                                  \
+  "s_waitcnt vmcnt(0)\n\t"                                 \
+  "s_branch 2f\n"                                           \
+  "1:\n\t"                                                 \
+  "s_waitcnt vmcnt(%[cnt])\n"                               \
+  "2:"
+template <int N>
+__device__ __forceinline__ void rq_vmwait_one(uint32_t first, vec16 (&v)[8]) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  const uint32_t fs = __builtin_amdgcn_readfirstlane(first);
+  asm volatile(QDC_RQ_WAIT_ASM
+               : "+{v[96:99]}"(v[0]), "+{v[100:103]}"(v[1]), "+{v[104:107]}"(v[2]), "+{v[108:111]}"(v[3]), "+{v[112:115]}"(v[4]), "+{v[116:119]}"(v[5]), "+{v[120:123]}"(v[6]), "+{v[124:127]}"(v[7])
+               : [first] "s"(fs), [cnt] "n"(N)
+               : "memory", "scc");
+}
+template <int N>
+__device__ __forceinline__ void rq_vmwait_two(uint32_t first, vec16 (&v)[8], vec16 (&w)[8]) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  const uint32_t fs = __builtin_amdgcn_readfirstlane(first);
+  asm volatile(QDC_RQ_WAIT_ASM
+               : "+{v[192:195]}"(v[0]), "+{v[196:199]}"(v[1]), "+{v[200:203]}"(v[2]), "+{v[204:207]}"(v[3]), "+{v[208:211]}"(v[4]), "+{v[212:215]}"(v[5]), "+{v[216:219]}"(v[6]), "+{v[220:223]}"(v[7]),
+                 "+{v[224:227]}"(w[0]), "+{v[228:231]}"(w[1]), "+{v[232:235]}"(w[2]), "+{v[236:239]}"(w[3]), "+{v[240:243]}"(w[4]), "+{v[244:247]}"(w[5]), "+{v[248:251]}"(w[6]), "+{v[252:255]}"(w[7])
+               : [first] "s"(fs), [cnt] "n"(N)
+               : "memory", "scc");
 }
 
 // TWO: fwd and bwd (reverse sweep, Gamma stages reduce into partials); else fwd only.
@@ -241,8 +316,7 @@ __device__ __forceinline__ void rq_exchange(cx (&x)[RQ_R], cx* buf, uint32_t tp,
 #define QDC_RQ_PF_WAVES 2  // waves/SIMD of the prefetching variant (state + next tile in VGPRs)
 #endif
 // PF: software pipeline — the next tile's chunks are loaded into registers while this tile's
-// stages run (2x the state registers, so fewer waves; no spills allowed: a scratch reload would
-// wait for the in-flight prefetch, vmcnt being in order).
+// stages run (2x the state registers, so fewer waves).
 template <bool TWO, int NT, bool PF>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF ? QDC_RQ_PF_WAVES : 4)))
 void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
@@ -332,9 +406,17 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     for (uint32_t j = 0; j < fg.nops; ++j) {
       const fop op = ops[j];
       const uint32_t kind = op.kind & 7u;
-      const bool gamma = TWO && (op.kind & FOP_GAMMA);
+      const bool gamma = TWO && (op.kind & FOP_GAMMA) && !(QDC_RQ_ABL & 4);
       const cx* M = mats + op.mat;
       real* acc = TWO ? &accw[wave][ri < FMAX_GRAD_RQ ? ri : 0][0] : nullptr;
+      if ((QDC_RQ_ABL & 2) && kind == FK_RELAYOUT) {
+        lcur = op.mat;
+        continue;
+      }
+      if ((QDC_RQ_ABL & 1) && kind != FK_RELAYOUT) {
+        if (TWO && (op.kind & FOP_GAMMA)) ++ri;
+        continue;
+      }
       if (kind == FK_RELAYOUT) {
         const rq_layout* Lc = reinterpret_cast<const rq_layout*>(mats + lcur);
         const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
@@ -390,24 +472,59 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       store(xf, xb, base);
     }
   } else {
-    // two register sets, ping-pong: tile tt+1 loads while tile tt runs
-    cx af[RQ_R], ab[RQ_R], bf[RQ_R], bb[RQ_R];
-    uint64_t base_a = count ? tile_base(tile0) : 0, base_b = 0;
-    if (count) load(af, ab, base_a);
-    for (uint32_t tt = 0; tt < count; tt += 2) {
-      if (tt + 1 < count) {
-        base_b = tile_base(tile0 + tt + 1);
-        load(bf, bb, base_b);
+    // the next tile's chunks (pf_f, pf_b) are in flight while this tile (xf, xb) runs
+    constexpr int NLD = TWO ? 2 * CPT : CPT;  // vector-memory ops per tile: loads = stores
+    vec16 pf_f[CPT], pf_b[CPT];
+    cx xf[RQ_R], xb[RQ_R];
+    auto issue = [&](uint64_t base) __attribute__((always_inline)) {
+      const rqio* rg = rqio_now();
+      const chunk* pf = f + (base + thr_ld);
+      const chunk* pb = b + (base + thr_ld);
+      constexpr int BASE = TWO ? RQ_PIN_TWO : RQ_PIN_ONE;
+#define QDC_RQ_ISSUE(i)                                                                   \
+  pf_f[i] = rq_ld<BASE + 4 * (i)>(pf + rg->offi_ld[i]);                                   \
+  if constexpr (TWO) pf_b[i] = rq_ld<RQ_PIN_TWO + 32 + 4 * (i)>(pb + rg->offi_ld[i]);
+      static_assert(CPT == 8, "eight chunks per state and thread");
+      QDC_RQ_ISSUE(0) QDC_RQ_ISSUE(1) QDC_RQ_ISSUE(2) QDC_RQ_ISSUE(3)
+      QDC_RQ_ISSUE(4) QDC_RQ_ISSUE(5) QDC_RQ_ISSUE(6) QDC_RQ_ISSUE(7)
+#undef QDC_RQ_ISSUE
+    };
+    auto take = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const chunk c = __builtin_bit_cast(chunk, pf_f[i]);
+        xf[2 * i] = c.v[0];
+        xf[2 * i + 1] = c.v[1];
+        if constexpr (TWO) {
+          const chunk d = __builtin_bit_cast(chunk, pf_b[i]);
+          xb[2 * i] = d.v[0];
+          xb[2 * i + 1] = d.v[1];
+        }
       }
-      run(af, ab);
-      store(af, ab, base_a);
-      if (tt + 1 >= count) break;
-      if (tt + 2 < count) {
-        base_a = tile_base(tile0 + tt + 2);
-        load(af, ab, base_a);
+    };
+    // Step s takes tile s-1 (loaded during step s-1), issues tile s, runs and stores tile s-1.
+    // One issue site: the in-flight registers are a loop-carried value with an undefined entry,
+    // so the register allocator has no phi copies to place (a copy before the wait would read
+    // in-flight registers; tools/check_rq_isa.py checks the ISA for exactly that).
+    uint64_t cur = 0;
+    for (uint32_t s = 0; s <= count; ++s) {
+      // younger than tile s-1's loads: tile s-2's stores (none before the second tile; at s = 0
+      // nothing is in flight and take() reads registers nothing uses).  Unconditional, so every
+      // path from an issue to the next read of its registers passes this wait.
+      if constexpr (TWO)
+        rq_vmwait_two<NLD>(s <= 1 ? 1u : 0u, pf_f, pf_b);
+      else
+        rq_vmwait_one<NLD>(s <= 1 ? 1u : 0u, pf_f);
+      take();
+      const uint64_t prev = cur;
+      if (s < count) {
+        cur = tile_base(tile0 + s);
+        issue(cur);
       }
-      run(bf, bb);
-      store(bf, bb, base_b);
+      if (s > 0) {
+        run(xf, xb);
+        store(xf, xb, prev);
+      }
     }
   }
   if constexpr (TWO) {

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 step() { echo "== $1"; }
 step tests
 timeout -k 10 900 python -m pytest tests -m gpu -q > "$OUT/tests.log" 2>&1
-rc=$?; tail -3 "$OUT/tests.log"; [ $rc -le 1 ] || exit $rc
+rc=$?; tail -3 "$OUT/tests.log"; [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
   step "pmc $c"
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o pmc \
