@@ -88,6 +88,23 @@ QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
   return nullptr;
 }
 
+// A range of one local shard in physical order (no qubit un-permutation): for streaming reads
+// of states too large for one host copy, e.g. the uncompute error of a 64 GiB state.
+QDC_API const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, size_t offset,
+                                          qdc_complex* host, size_t len) {
+  qdc::Circuit& k = c->impl;
+  if (shard < 0 || (size_t)shard >= k.sh.size()) return qdc::fail("no local shard %d", shard);
+  const size_t size = (size_t)1 << k.nl;
+  if (offset > size || len > size - offset) return qdc::fail("range out of the shard");
+  const qdc::Shard& s = k.sh[shard];
+  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
+  if (!src) return qdc::fail("state %d is not allocated", which);
+  QDC_HIP(hipMemcpyAsync(host, src + offset, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
+                         k.ctx.stream));
+  QDC_HIP(hipStreamSynchronize(k.ctx.stream));
+  return nullptr;
+}
+
 // Unsharded circuits only (a sharded state is assembled from qdc_circuit_get_shard + layout).
 QDC_API const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex* host,
                                           size_t len) {
@@ -297,6 +314,7 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
 QDC_API size_t qdc_rq_plan(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
                            const unsigned* t2, const unsigned long long* deps, size_t n,
                            unsigned* steps, size_t cap) {
+  if (n > 64) return SIZE_MAX;  // rq_plan's stage sets are 64-bit masks (passes hold <= FMAX_OPS)
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
   const char* mc = getenv("QDC_RQ_MAXCL");  // the runtime's knob (qdc_circuit.hpp)

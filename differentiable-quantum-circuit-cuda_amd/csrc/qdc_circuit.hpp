@@ -665,6 +665,15 @@ struct Circuit {
       if (!it.swaps.empty() && !rq)
         return fail("internal: a permuting fused pass is not register-resident");
       it.tbits = (uint32_t)LV + it.lc + it.h;
+      // the kernels index their per-wave accumulators by reduction op: a pass with more
+      // reduction ops than accumulators is a planner bug, never folded into another slot
+      {
+        const size_t nred = it.grad_slots.size();
+        const size_t cap = rq ? (size_t)FMAX_GRAD_RQ : (size_t)FMAX_GRAD;
+        if (nred > cap)
+          return fail("internal: a fused pass has %zu reduction ops, the kernel holds %zu", nred,
+                      cap);
+      }
       if (!rq) {
         for (const fop& F : pf) fops[fo++] = F;
         it.nstage = (uint32_t)pf.size();

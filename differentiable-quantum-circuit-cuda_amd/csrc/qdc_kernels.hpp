@@ -558,6 +558,8 @@ constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (>= its gradient
 // C2 n=28: 24 / 32 give 20 % / 15 % fewer reverse passes, each 33 % / 23 % slower (more
 // relayouts per stage, 7 / 6 blocks per CU): 16 is best.
 constexpr int FMAX_GRAD_RQ = QDC_FMAX_GRAD_RQ;
+static_assert(FMAX_GRAD_RQ >= 1 && FMAX_GRAD >= 1, "at least one reduction accumulator");
+static_assert(FMAX_OPS <= 64, "rq_plan keeps stage sets in 64-bit masks");
 constexpr int FMAX_ROWS = 8;   // far qubits per tile
 constexpr int FACC = 32;       // reals per gradient accumulator (16 complex)
 

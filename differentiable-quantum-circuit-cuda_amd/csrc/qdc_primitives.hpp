@@ -1,10 +1,12 @@
 // qdc_primitives.hpp — the 18 reference C-ABI entry points (src/primitives_bind.rs:15-119,
 // implemented for CUDA in src/primitives.cu:141-953) on the HIP kernels.
 //
-// All calls share one process-wide context on the device that was current at first use:
-// one non-blocking stream, ordered exactly like the reference's legacy default stream; host
-// results (copies, densities, gradients) synchronise it.  A mutex makes concurrent callers
-// safe (the reference's are not, README.md:13).
+// Every call runs on a context of the device that is current for the calling thread (as the
+// reference launches on the current device's legacy default stream): one non-blocking stream
+// per device, ordered exactly like that default stream; host results (copies, densities,
+// gradients) synchronise it.  A host that switches devices (hipSetDevice) between calls, or
+// drives one GPU per thread, gets each device's own stream and scratch.  A mutex makes
+// concurrent callers safe (the reference's are not, README.md:13).
 #pragma once
 
 #include "qdc/circuit.h"
@@ -19,20 +21,23 @@ inline std::mutex& abi_mutex() {
   return m;
 }
 
+constexpr int ABI_MAX_DEVICES = 64;
+
 inline const char* abi_ctx(Ctx*& out) {
-  static Ctx* ctx = nullptr;
-  if (!ctx) {
-    int dev = 0;
-    QDC_HIP(hipGetDevice(&dev));
+  static Ctx* ctx[ABI_MAX_DEVICES] = {};
+  int dev = 0;
+  QDC_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= ABI_MAX_DEVICES) return fail("device %d is out of the supported range", dev);
+  if (!ctx[dev]) {
     Ctx* c = new Ctx();
     const char* e = c->init(dev);
     if (e) {
       delete c;
       return e;
     }
-    ctx = c;
+    ctx[dev] = c;
   }
-  out = ctx;
+  out = ctx[dev];
   return nullptr;
 }
 
@@ -305,10 +310,9 @@ __attribute__((visibility("default"))) const char* qdc_qkgate(qdc_complex* state
     for (size_t c = 0; c < b; ++c)
       if (pos[c] == pos[b]) return qdc::fail("positions must be different.");
   }
-  static qdc::real* buf = nullptr;  // guarded by the ABI mutex
-  static size_t cap = 0;
+  static qdc::QkRing rings[qdc::ABI_MAX_DEVICES];  // guarded by the ABI mutex
   return qdc::apply_qk(ctx, reinterpret_cast<qdc::cx*>(state), gate, pos, (uint32_t)k,
-                       (uint32_t)n, buf, cap);
+                       (uint32_t)n, rings[ctx.device]);
 }
 
 __attribute__((visibility("default"))) const char* qdc_abi_sync(void) {

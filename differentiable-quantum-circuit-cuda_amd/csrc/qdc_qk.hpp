@@ -122,12 +122,39 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
 
 namespace qdc {
 
+// Operand uploads without host syncs: a ring of device slots, each with a pinned staging slot
+// and an event recorded after the launch that reads it; a slot is rewritten only once that
+// launch is done (hipEventSynchronize, which returns at once unless the GPU is QK_RING calls
+// behind).
+constexpr int QK_RING = 8;
+struct QkRing {
+  real* dev[QK_RING] = {};
+  real* host[QK_RING] = {};
+  hipEvent_t done[QK_RING] = {};
+  size_t cap = 0;  // reals per slot
+  int next = 0;
+  const char* reserve(size_t n) {
+    if (n <= cap) return nullptr;
+    for (int i = 0; i < QK_RING; ++i) {
+      if (done[i]) QDC_HIP(hipEventSynchronize(done[i]));
+      if (dev[i]) QDC_HIP(hipFree(dev[i]));
+      if (host[i]) QDC_HIP(hipHostFree(host[i]));
+      dev[i] = nullptr;
+      host[i] = nullptr;
+      QDC_HIP(hipMalloc(&dev[i], n * sizeof(real)));
+      QDC_HIP(hipHostMalloc(&host[i], n * sizeof(real)));
+      if (!done[i]) QDC_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+    }
+    cap = n;
+    return nullptr;
+  }
+};
+
 // Dense k-qubit gate on a state (k = 1, 2 route to the single-gate kernels).  `U` is the
 // host gate (C×C row-major), `pos` the k target qubits (pos[0] most significant).  The
-// operand buffer is device memory owned by the caller, grown here; the call synchronises the
-// stream around its upload (the reference uploads every gate with cudaMemcpyToSymbol too).
+// operands go through the ring (read by the device before the host can touch the slot again).
 inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* pos, uint32_t k,
-                            uint32_t n, real*& buf, size_t& cap) {
+                            uint32_t n, QkRing& ring) {
   if (k == 1) return apply_dense<2>(c, s, to_mat<2>(U), (uint32_t)pos[0], (uint32_t)pos[0], n, "qk1");
   if (k == 2)
     return apply_dense<4>(c, s, to_mat<4>(U), (uint32_t)pos[0], (uint32_t)pos[1], n, "qk2");
@@ -149,23 +176,26 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
       if ((ci >> (k - 1 - b)) & 1u) o |= (uint64_t)1 << pos[b];
     g.off[ci] = o;
   }
-  QDC_HIP(hipStreamSynchronize(c.stream));  // the previous qk launch is done with buf
-  if (a.size() > cap) {
-    if (buf) QDC_HIP(hipFree(buf));
-    buf = nullptr;
-    QDC_HIP(hipMalloc(&buf, a.size() * sizeof(real)));
-    cap = a.size();
-  }
-  QDC_HIP(hipMemcpyAsync(buf, a.data(), a.size() * sizeof(real), hipMemcpyHostToDevice, c.stream));
-  QDC_HIP(hipStreamSynchronize(c.stream));
+  QDC_TRY(ring.reserve((size_t)(QK_MAX == 5 ? (32 / 8) * (32 / 2) * 64 : a.size())));
+  const int slot = ring.next;
+  ring.next = (ring.next + 1) % QK_RING;
+  QDC_HIP(hipEventSynchronize(ring.done[slot]));  // the launch that last read this slot is done
+  std::memcpy(ring.host[slot], a.data(), a.size() * sizeof(real));
+  QDC_HIP(hipMemcpyAsync(ring.dev[slot], ring.host[slot], a.size() * sizeof(real),
+                         hipMemcpyHostToDevice, c.stream));
   const uint64_t nb = k == 3 ? 4 : k == 4 ? 2 : 1;  // batches per wave iteration (k_qk)
   const uint64_t waves = ((g.ngroups + 15) / 16 + nb - 1) / nb;
   const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 256u * 16u);
   c.next_flops = 8.0 * C * (double)((uint64_t)1 << n);  // C complex MACs per amplitude
   const double bytes = 2.0 * state_bytes(n);
-  if (k == 3) return c.launch_block("qk3", bytes, k_qk<3>, grid, 256u, s, buf, g);
-  if (k == 4) return c.launch_block("qk4", bytes, k_qk<4>, grid, 256u, s, buf, g);
-  return c.launch_block("qk5", bytes, k_qk<5>, grid, 256u, s, buf, g);
+  const real* buf = ring.dev[slot];
+  const char* e;
+  if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3>, grid, 256u, s, buf, g);
+  else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4>, grid, 256u, s, buf, g);
+  else e = c.launch_block("qk5", bytes, k_qk<5>, grid, 256u, s, buf, g);
+  QDC_TRY(e);
+  QDC_HIP(hipEventRecord(ring.done[slot], c.stream));
+  return nullptr;
 }
 
 }  // namespace qdc

@@ -408,7 +408,8 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       const uint32_t kind = op.kind & 7u;
       const bool gamma = TWO && (op.kind & FOP_GAMMA) && !(QDC_RQ_ABL & 4);
       const cx* M = mats + op.mat;
-      real* acc = TWO ? &accw[wave][ri < FMAX_GRAD_RQ ? ri : 0][0] : nullptr;
+      // ri < FMAX_GRAD_RQ: build_program rejects a pass with more Gamma stages
+      real* acc = TWO ? &accw[wave][ri][0] : nullptr;
       if ((QDC_RQ_ABL & 2) && kind == FK_RELAYOUT) {
         lcur = op.mat;
         continue;

@@ -197,6 +197,12 @@ class _CircuitBase:
         check(self._lib.qdc_circuit_get_shard(self._h, which, shard, ptr(out), out.size))
         return out
 
+    def get_range(self, which: int, offset: int, count: int, shard: int = 0) -> np.ndarray:
+        """`count` amplitudes of a local shard from `offset`, in PHYSICAL order (see layout())."""
+        out = np.empty(count, dtype=self._dtype)
+        check(self._lib.qdc_circuit_get_range(self._h, which, shard, offset, ptr(out), count))
+        return out
+
     def get_state(self, which: int = 0) -> np.ndarray:
         """Copy of the forward (0), initial (1) or backward (2) state in logical qubit order.
         Sharded over processes: the local shards are gathered with torch.distributed."""

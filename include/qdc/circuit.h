@@ -142,6 +142,11 @@ const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world,
 const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard, qdc_complex* host,
                                   size_t len);
 
+/* A range [offset, offset + len) of one local shard in PHYSICAL order (qubits may be permuted:
+ * qdc_circuit_layout); for streaming reads of states too large for one host copy. */
+const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, size_t offset,
+                                  qdc_complex* host, size_t len);
+
 /* ---- the sharding planner (host only, no GPU) ---------------------------------------- */
 enum qdc_plan_mode { QDC_PLAN_RUN = 0, QDC_PLAN_FORWARD = 1, QDC_PLAN_BACKWARD = 2 };
 enum qdc_plan_type { QDC_PLAN_OP = 0, QDC_PLAN_REMAP = 1 };

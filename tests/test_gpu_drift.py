@@ -1,0 +1,181 @@
+"""Depth, drift and the U[out, in] convention on the GPU.
+
+* BASELINE config C5 at its stated depth: a 10 000-gate deep random circuit (50 % Haar q1, 35 %
+  Haar q2, 15 % diagonal) fwd + bwd at n = 14 against the complex128 oracle, f32 and f64, within
+  4x the measured floor of the reference's own algorithm (tests/floors.py) for every output:
+  densities, gradients, the forward state, the uncomputed state after the O(1)-memory reverse
+  sweep (src/circuit.rs:266-429 uncomputes with U^dagger at every gate: SURVEY.md §7 hard part
+  (ii)) and the final cotangent state.
+* The same 10 000 gates at the full n = 33 on one GPU (three 64 GiB states): density
+  invariants, the uncompute error |psi after backward - psi_0| read back in streaming chunks,
+  and the finite-difference identity dL = sum_k Re(G_k . P_k) (test_autodiff.py:121-165) along a
+  direction on the gates nearest the measured qubits.
+* A known-answer test with deliberately non-symmetric matrices: every reference KAT uses
+  symmetric gates (Hadamard, CNOT, CZ, pr.cu:968-978), so the row-major U[out, in] convention
+  (quantized_tensor.rs:293: out[p] = sum_q U[2p + q] in[q]) and the gradient / density index
+  order were pinned only by transcription; here they are checked against hand-computed values.
+"""
+import gc
+import time
+
+import numpy as np
+import pytest
+
+import floors as F
+from quantum_differentiable_circuit import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def build(prec, n, ins, **kw):
+    import quantum_differentiable_circuit as q
+    c = q.circuit_class(prec)(n, **kw)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    return c
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_c5_depth_10k_gates_vs_oracle(prec):
+    n = 14
+    ins, var = W.deep_random_circuit(n, 10000, seed=33)
+    fl = F.Floor(prec, n, ins, [], var, run=False)
+    c = build(prec, n, ins)
+    fl.check("forward", c.forward([], fl.var), f"C5 n={n} 10k {prec} ")
+    fl.check("state", c.get_state(0), f"C5 n={n} 10k {prec} ")
+    fl.check("grads", c.backward(fl.cots, [], fl.var), f"C5 n={n} 10k {prec} ")
+    psi = c.get_state(0)
+    fl.check("uncomputed", psi, f"C5 n={n} 10k {prec} ")
+    fl.check("bwd", c.get_state(2), f"C5 n={n} 10k {prec} ")
+    e0 = np.zeros_like(psi)
+    e0[0] = 1
+    print(f"[drift] C5 n={n} 10k {prec}: |psi after backward - psi0| = "
+          f"{np.linalg.norm(psi.astype(np.complex128) - e0):.3e}")
+    if prec == "f64":
+        assert F.normrel(c.backward(fl.cots, [], fl.var), fl.exact["grads"]) <= 1e-10
+
+
+def _stream_uncompute_error(c, n, chunk=1 << 26):
+    """|psi - |0..0>| of the fwd state, read in chunks (index 0 is |0..0> in every qubit
+    permutation of the physical layout)."""
+    s = 0.0
+    for off in range(0, 1 << n, chunk):
+        x = c.get_range(0, off, min(chunk, (1 << n) - off)).astype(np.complex128)
+        if off == 0:
+            x[0] -= 1
+        s += float(np.vdot(x, x).real)
+    return np.sqrt(s)
+
+
+def test_c5_full_size_10k_gates():
+    n, ngates = 33, 10000
+    ins, var = W.deep_random_circuit(n, ngates, seed=33)
+    vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
+    c = build("f32", n, ins)
+    t0 = time.perf_counter()
+    d = c.forward([], vg)
+    t1 = time.perf_counter()
+    assert len(d) == 4
+    for x in d:
+        assert abs(np.trace(x) - 1) < 1e-4
+        assert np.abs(x - x.conj().T).max() < 1e-5
+        assert np.linalg.eigvalsh((x + x.conj().T) / 2).min() > -1e-4
+    cots = F.sigma_z_cots(d, np.complex64)
+    g = c.backward(cots, [], vg)
+    t2 = time.perf_counter()
+    assert all(np.isfinite(x).all() for x in g)
+    drift = _stream_uncompute_error(c, n)
+    print(f"[drift] C5 n={n} {ngates} gates f32: forward {t1 - t0:.1f} s, backward {t2 - t1:.1f} s, "
+          f"|psi after backward - psi0| = {drift:.3e}")
+    # 10k f32 uncomputations: the C restatement of the reference drifts 1.5e-7 at n = 14
+    # (tests/floors.py, 10k gates); allow for n = 33's longer reductions and sqrt(2^n) spread
+    assert drift < 1e-4
+    # finite differences along the 48 variable gates nearest the output (their gradients are
+    # O(1); deep in a 10k-gate random circuit they are exponentially small, below f32 noise)
+    rng = np.random.default_rng(5)
+    chosen = range(len(vg) - 48, len(vg))  # every gate of the C5 generator is variable
+    p = [np.zeros_like(x) for x in vg]
+    for i in chosen:
+        p[i] = (rng.standard_normal(vg[i].shape) + 1j * rng.standard_normal(vg[i].shape)).astype(
+            np.complex64)
+
+    def loss(gates):
+        return sum(np.real(np.trace(x.astype(np.complex128) @ np.diag([1.0, -1.0])))
+                   for x in c.forward([], gates))
+
+    eps = 1e-2
+    lp = loss([(x + eps * y).astype(np.complex64) for x, y in zip(vg, p)])
+    lm = loss([(x - eps * y).astype(np.complex64) for x, y in zip(vg, p)])
+    fd = (lp - lm) / (2 * eps)
+    an = sum(np.real(np.sum(g[i].astype(np.complex128) * p[i].reshape(-1))) for i in chosen)
+    scale = np.linalg.norm(np.concatenate([g[i] for i in chosen])) * np.linalg.norm(
+        np.concatenate([p[i].reshape(-1) for i in chosen]))
+    print(f"[fd] C5 n={n}: finite difference {fd:.6e}, analytic {an:.6e}, scale {scale:.3e}")
+    assert abs(fd - an) <= 2e-3 * scale, (fd, an, scale)
+    del c
+    gc.collect()
+
+
+# --- non-symmetric known answers (hand-computed from primitives.cu:513-606, 202-292, 689-837) --
+A2 = np.array([1 + 2j, 3 - 1j, -2 + 0.5j, 0.25 + 4j])  # U = [[a, b], [c, d]], b != c
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_nonsymmetric_kat_q1_gate_density_grad(prec):
+    import quantum_differentiable_circuit as q
+    dt = F.DT[prec]
+    n, pos = 4, 2
+    t = q.QuantizedTensor.new_standard(n, prec)
+    t.apply_q1_gate(A2.astype(dt), pos)
+    psi = t.get_cpu_state_copy()
+    want = np.zeros(1 << n, np.complex128)
+    want[0] = A2[0]            # out[0] = U[0] in[0]
+    want[1 << pos] = A2[2]     # out[1] = U[2] in[0]: row-major U[out, in], not U[1]
+    assert np.abs(psi - want).max() < 1e-6
+    rho = t.get_q1_density(pos)  # rho[2p + q] = sum psi_p conj(psi_q)
+    assert np.abs(rho - np.array([abs(A2[0]) ** 2, A2[0] * np.conj(A2[2]),
+                                  A2[2] * np.conj(A2[0]), abs(A2[2]) ** 2])).max() < 1e-5
+    # q1grad: G[2p + q] = sum_b bwd[b + p 2^pos] fwd[b + q 2^pos], fwd = |0>, bwd = |1 on pos>
+    fwd = q.QuantizedTensor.new_standard(n, prec)
+    bwd_h = np.zeros(1 << n, dt)
+    bwd_h[1 << pos] = 1
+    bwd = q.QuantizedTensor.new_from_host(bwd_h, prec)
+    g = q.get_q1_grad(fwd, bwd, pos)
+    assert np.abs(g - np.array([0, 0, 1, 0])).max() == 0  # entry (p = 1, q = 0)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_nonsymmetric_kat_q2_gate_pos2_is_msb(prec):
+    import quantum_differentiable_circuit as q
+    dt = F.DT[prec]
+    n, pos2, pos1 = 5, 3, 1
+    u = (np.arange(16) + 1) * (1 + 0.5j)  # U[8 Q2 + 4 Q1 + 2 P2 + P1], far from symmetric
+    t = q.QuantizedTensor.new_standard(n, prec)
+    t.apply_q2_gate(u.astype(dt), pos2, pos1)
+    psi = t.get_cpu_state_copy()
+    want = np.zeros(1 << n, np.complex128)
+    # in = |P2 = 0, P1 = 0>: out[2 Q2 + Q1] = U[4 (2 Q2 + Q1)] at index Q2 2^pos2 + Q1 2^pos1
+    for q2 in (0, 1):
+        for q1 in (0, 1):
+            want[(q2 << pos2) | (q1 << pos1)] = u[8 * q2 + 4 * q1]
+    assert np.abs(psi - want).max() < 1e-5 * np.abs(u).max()
+    # the circuit runtime on the same gate as a constant gate, unfused (n = 5) and in a fused
+    # register-resident pass (n = 13, two gates + a density in one tile)
+    for nn in (5, 13):
+        u1 = A2.astype(dt)
+        c = build(prec, nn, [(6, (pos1,)), (0, (pos2, pos1)), (11, (pos1,)), (10, (pos2, pos1))])
+        r1, r2 = c.run([np.eye(2, dtype=dt).reshape(-1), u.astype(dt)], [])
+        s = np.zeros(1 << nn, np.complex128)
+        for q2 in (0, 1):
+            for q1 in (0, 1):
+                s[(q2 << pos2) | (q1 << pos1)] = u[8 * q2 + 4 * q1]
+        m = s.reshape((2,) * nn)  # axis k = qubit nn - 1 - k
+        ax = [nn - 1 - pos2, nn - 1 - pos1]
+        t2 = np.moveaxis(m, ax, [0, 1]).reshape(4, -1)
+        rho2 = t2 @ t2.conj().T  # rho[2 p2 + p1, 2 q2 + q1] (pos2 the MSB)
+        rho1 = np.array([[rho2[0, 0] + rho2[2, 2], rho2[0, 1] + rho2[2, 3]],
+                         [rho2[1, 0] + rho2[3, 2], rho2[1, 1] + rho2[3, 3]]])
+        scale = np.abs(rho2).max()
+        assert np.abs(r1 - rho1).max() < 1e-5 * scale, nn
+        assert np.abs(r2 - rho2).max() < 1e-5 * scale, nn
+        del u1

@@ -1,12 +1,13 @@
 """The HIP path against the committed golden fixtures (tests/golden/*.npz, made by
 tests/golden/make_golden.py from the oracle).  Tolerances: 1e-5 (f32) / 1e-12 (f64) in the
 reference's per-element metric for single ops (test_utils.rs:20-42), norm-relative for
-reductions and multi-gate circuits."""
+reductions; multi-gate circuits within 4x the measured floor (tests/floors.py)."""
 from pathlib import Path
 
 import numpy as np
 import pytest
 
+import floors as F
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -57,22 +58,30 @@ def test_golden_primitives(prec):
 @pytest.mark.parametrize("name", ["circuit_autodiff", "circuit_layered"])
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 def test_golden_circuits(name, prec):
+    """The fixtures hold complex128 results of the fixture-precision inputs; the HIP path must
+    be within 4x the floor of the reference's own algorithm on the same inputs (the C
+    restatement of its kernels in `prec`, tests/floors.py)."""
     import quantum_differentiable_circuit as q
     z = np.load(GOLDEN / f"{name}_{prec}.npz")
     n = int(z["n"])
+    ins = [(int(k), (int(a), int(b)) if int(k) in Q2_KINDS else (int(a),))
+           for k, a, b in z["instructions"]]
     c = q.circuit_class(prec)(n)
-    for k, a, b in z["instructions"]:
-        c._push(int(k), int(a), int(b) if int(k) in Q2_KINDS else 0)
+    for kind, pos in ins:
+        c._push(kind, *pos)
     c.set_state_from_vector(z["psi0"])
     const, var = split(z["const"], z["const_lens"]), split(z["var"], z["var_lens"])
-    tol = TOL[prec] * 20  # ~100-gate circuits incl. non-unitary gates
-    run = c.run(const, var)
-    assert normrel(np.concatenate([r.reshape(-1) for r in run]), z["run"]) < tol
-    fwd = c.forward(const, var)
-    assert normrel(np.concatenate([r.reshape(-1) for r in fwd]), z["forward"]) < tol
     cots = [x.reshape(int(np.sqrt(x.size)), -1) for x in split(z["cotangents"], z["cotangent_lens"])]
+    fl = F.Floor(prec, n, ins, const, var, psi0=z["psi0"], cots=lambda d, dt: cots)
+    # the fixtures are the exact results (rounded to `prec`) the floor is measured against
+    for key, fix in (("run", "run"), ("forward", "forward"), ("grads", "grads"),
+                     ("uncomputed", "final_state"), ("bwd", "final_bwd")):
+        assert F.normrel(fl.exact[key], z[fix]) < (1.2e-7 if prec == "f32" else 1e-14), key
+    what = f"golden {name} {prec} "
+    fl.check("run", c.run(const, var), what)
+    fl.check("forward", c.forward(const, var), what)
     grads = c.backward(cots, const, var)
     assert [g.size for g in grads] == list(z["grad_lens"])
-    assert normrel(np.concatenate(grads), z["grads"]) < tol * 10
-    assert normrel(c.get_state(0), z["final_state"]) < tol * 10
-    assert normrel(c.get_state(2), z["final_bwd"]) < tol * 10
+    fl.check("grads", grads, what)
+    fl.check("uncomputed", c.get_state(0), what)
+    fl.check("bwd", c.get_state(2), what)

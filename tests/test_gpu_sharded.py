@@ -11,6 +11,7 @@ import socket
 import numpy as np
 import pytest
 
+import floors as F
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -35,32 +36,18 @@ def test_local_shards_match_oracle(prec, shards):
     import quantum_differentiable_circuit as q
     n = 11
     ins, const, var, _ = O.autodiff_circuit(n, 2, seed=17)
-    dt = DT[prec]
-    cg = [g.astype(dt) for g in const]
-    vg = [g.astype(dt) for g in var]
-    psi0 = O.random_state(np.random.default_rng(2), n).astype(dt)
+    psi0 = O.random_state(np.random.default_rng(2), n)
+    fl = F.Floor(prec, n, ins, const, var, psi0=psi0, cots=F.tsallis_cots)
     c = build(q, prec, n, ins, local_shards=shards)
-    c.set_state_from_vector(psi0)
-    o = O.OracleCircuit(n, dt)
-    for kind, pos in ins:
-        o.add(kind, *pos)
-    o.set_state_from_vector(psi0)
-    tol = 2e-4 if prec == "f32" else 1e-11
-    got_run, want_run = c.run(cg, vg), o.run(cg, vg)
-    assert normrel(np.concatenate([d.reshape(-1) for d in got_run]),
-                   np.concatenate([d.reshape(-1) for d in want_run])) < tol
-    got, want = c.forward(cg, vg), o.forward(cg, vg)
-    assert normrel(np.concatenate([d.reshape(-1) for d in got]),
-                   np.concatenate([d.reshape(-1) for d in want])) < tol
+    c.set_state_from_vector(fl.psi0)
+    what = f"autodiff n={n} {prec} {shards} shards "
+    fl.check("run", c.run(fl.const, fl.var), what)
+    fl.check("forward", c.forward(fl.const, fl.var), what)
     phys, world, _, nloc = c.layout()
     assert world == shards and nloc == shards
-    assert normrel(c.get_state(0), o.state) < tol  # forward final state, un-permuted
-    _, cots = O.tsallis_loss_and_cotangents([d.astype(np.complex128) for d in want])
-    cots = [np.ascontiguousarray(x.conj(), dtype=dt) for x in cots]
-    g_got = np.concatenate(c.backward(cots, cg, vg))
-    g_want = np.concatenate(o.backward(cots, cg, vg))
-    assert normrel(g_got, g_want) < tol * 10
-    assert normrel(c.get_state(0), o.state) < tol * 10
+    fl.check("state", c.get_state(0), what)  # forward final state, un-permuted
+    fl.check("grads", c.backward(fl.cots, fl.const, fl.var), what)
+    fl.check("uncomputed", c.get_state(0), what)
 
 
 def test_local_shards_equal_unsharded_on_brickwork():
@@ -68,16 +55,15 @@ def test_local_shards_equal_unsharded_on_brickwork():
     import quantum_differentiable_circuit as q
     n = 16
     ins, var = O.layered_circuit(n, 3, seed=33)
-    vg = [g.astype(np.complex64) for g in var]
+    fl = F.Floor("f32", n, ins, [], var, run=False)
     a = build(q, "f32", n, ins)
     b = build(q, "f32", n, ins, local_shards=8)
-    da, db = a.forward([], vg), b.forward([], vg)
-    assert normrel(np.concatenate([d.reshape(-1) for d in db]),
-                   np.concatenate([d.reshape(-1) for d in da])) < 1e-5
-    cots = [np.diag([1.0, -1.0]).astype(np.complex64) for _ in da]
-    ga, gb = np.concatenate(a.backward(cots, [], vg)), np.concatenate(b.backward(cots, [], vg))
-    assert normrel(gb, ga) < 1e-5
-
+    da, db = a.forward([], fl.var), b.forward([], fl.var)
+    fl.check("forward", db, "C2 n=16 8 shards ")
+    F.check_pair("f32", db, da, fl.floor["forward"], "C2 n=16 8 shards vs unsharded forward")
+    ga, gb = a.backward(fl.cots, [], fl.var), b.backward(fl.cots, [], fl.var)
+    fl.check("grads", gb, "C2 n=16 8 shards ")
+    F.check_pair("f32", gb, ga, fl.floor["grads"], "C2 n=16 8 shards vs unsharded grads")
 
 def _free_port():
     s = socket.socket()

@@ -240,3 +240,40 @@ def test_qk_oracle_extends_q1_q2_conventions():
     u = np.kron(np.kron(a.reshape(2, 2), b.reshape(2, 2)), c.reshape(2, 2))
     want = O.apply_q1_gate(O.apply_q1_gate(O.apply_q1_gate(psi, a, 4), b, 0), c, 6)
     assert np.abs(O.apply_qk_gate(psi, u.reshape(-1), [4, 0, 6]) - want).max() < 1e-14
+
+
+# --- non-symmetric known answers: every reference KAT uses symmetric matrices (pr.cu:968-978),
+# so the row-major U[out, in] convention (quantized_tensor.rs:293), the pos2-MSB quartet order
+# (pr.cu:573-606) and the gradient index order (pr.cu:202-292) are pinned here by hand-computed
+# values, for both restatements (einsum oracle and the C kernels).
+def _kat_ops():
+    from oracle.cref import CRefOps
+    return [("einsum", O.EinsumOps, np.complex128), ("cref64", CRefOps("f64"), np.complex128),
+            ("cref32", CRefOps("f32"), np.complex64)]
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_nonsymmetric_kat_conventions(which):
+    name, ops, dt = _kat_ops()[which]
+    u2 = np.array([1 + 2j, 3 - 1j, -2 + 0.5j, 0.25 + 4j], dt)
+    n, pos = 4, 2
+    s = np.zeros(1 << n, dt)
+    s[0] = 1
+    out = ops.apply_q1_gate(s.copy(), u2, pos)
+    assert out[0] == u2[0] and out[1 << pos] == u2[2], name  # out[1] = U[2] in[0]
+    rho = ops.get_q1_density(out, pos)
+    np.testing.assert_allclose(rho, [abs(u2[0]) ** 2, u2[0] * np.conj(u2[2]),
+                                     u2[2] * np.conj(u2[0]), abs(u2[2]) ** 2], rtol=1e-6)
+    bwd = np.zeros(1 << n, dt)
+    bwd[1 << pos] = 1
+    g = ops.get_q1_grad(s.copy(), bwd, pos)
+    np.testing.assert_array_equal(g, [0, 0, 1, 0])  # G[2p + q], p = bwd's bit, q = fwd's
+    u4 = ((np.arange(16) + 1) * (1 + 0.5j)).astype(dt)
+    n, pos2, pos1 = 5, 3, 1
+    s = np.zeros(1 << n, dt)
+    s[0] = 1
+    out = ops.apply_q2_gate(s.copy(), u4, pos2, pos1)
+    for q2 in (0, 1):
+        for q1 in (0, 1):
+            assert out[(q2 << pos2) | (q1 << pos1)] == u4[8 * q2 + 4 * q1], (name, q2, q1)
+    assert np.count_nonzero(out) == 4
