@@ -120,31 +120,127 @@ def select_device(local):
         raise RuntimeError(f"hipSetDevice({local}) failed: {err}")
 
 
-def cpu_baseline(args, n):
-    """Time the oracle's C/OpenMP restatement of the reference algorithm (unfused uncompute /
-    grad / pull-back and allocate-conj-gate-add density injection, circuit.rs:266-429) on a
-    bounded sample of the same workload: its first `cpu_gates` gates and `cpu_densities`
-    DiffQ1Density outputs, at full n."""
-    from oracle import oracle as O
-    from oracle.cref import CRefOps
-    ops = CRefOps(args.precision)
-    ins, var = O.layered_circuit(n, args.layers, args.seed)
-    gates = [(k, p) for k, p in ins if k < 10][:args.cpu_gates]
-    dens_ins = [(k, p) for k, p in ins if k >= 10][:args.cpu_densities]
+def _cref_op_costs(ops, n, q1_pos, q2_pairs, dens1_pos, dens2_pairs, diag_pairs=()):
+    """Seconds per gate kind of the reference algorithm (src/circuit.rs:164-429 over
+    src/primitives.cu's kernels, restated in oracle/cpu_ref.c) on 2^n-amplitude host states:
+    a gate forward (1 apply) + backward (uncompute, gradient reduction, pull-back); a density
+    forward (1 reduction) + backward (conj_and_double into a new state, transposed apply, add).
+    Means over the sampled positions."""
+    from quantum_differentiable_circuit import workloads as W
     dt = ops.state_dtype
-    o = O.OracleCircuit(n, dt, ops=ops)
-    for kind, pos in gates + dens_ins:
-        o.add(kind, *pos)
-    var = var[:len(gates)]
-    t0 = time.perf_counter()
-    dens = o.forward([], var)
-    o.backward(sigma_z_cotangents(len(dens), dt), [], var)
-    dt_s = time.perf_counter() - t0
-    return {"value": len(gates) / dt_s, "unit": "gate-applications/s (fwd+bwd)",
-            "cores": ops.threads(), "kind": "port",
-            "sample": f"first {len(gates)} gates + {len(dens)} DiffQ1Density of the same "
-                      f"circuit at n={n} {args.precision}, fwd+bwd in {dt_s:.1f} s "
-                      f"(oracle/cpu_ref.c, OpenMP, reference algorithm unfused)"}
+    rng = np.random.default_rng(0)
+    f = np.empty(1 << n, dt)
+    f.real = rng.standard_normal(1 << n)
+    f.imag = rng.standard_normal(1 << n)
+    b = f[::-1].copy()
+    u2 = W.haar_unitary(rng, 2).astype(dt).reshape(-1)
+    u4 = W.haar_unitary(rng, 4).astype(dt).reshape(-1)
+    d4 = np.exp(1j * rng.standard_normal(4)).astype(dt)
+    u2h, u2t = np.conj(u2.reshape(2, 2).T).reshape(-1), u2.reshape(2, 2).T.reshape(-1).copy()
+    u4h, u4t = np.conj(u4.reshape(4, 4).T).reshape(-1), u4.reshape(4, 4).T.reshape(-1).copy()
+
+    def timed(fn):
+        t0 = time.perf_counter()
+        fn()
+        return time.perf_counter() - t0
+
+    out = {}
+
+    def q1(p):
+        ops.apply_q1_gate(f, u2, p)
+        ops.apply_q1_gate(f, u2h, p)
+        ops.get_q1_grad(f, b, p)
+        ops.apply_q1_gate(b, u2t, p)
+
+    def q2(pr):
+        ops.apply_q2_gate(f, u4, *pr)
+        ops.apply_q2_gate(f, u4h, *pr)
+        ops.get_q2_grad(f, b, *pr)
+        ops.apply_q2_gate(b, u4t, *pr)
+
+    def diag(pr):
+        ops.apply_q2_gate_diag(f, d4, *pr)
+        ops.apply_q2_gate_diag(f, np.conj(d4), *pr)
+        ops.get_q2_grad_diag(f, b, *pr)
+        ops.apply_q2_gate_diag(b, d4, *pr)
+
+    def dens1(p):
+        ops.get_q1_density(f, p)
+        add = ops.conj_and_double(f)
+        ops.apply_q1_gate(add, u2t, p)
+        ops.add(add, b)
+
+    def dens2(pr):
+        ops.get_q2_density(f, *pr)
+        add = ops.conj_and_double(f)
+        ops.apply_q2_gate(add, u4t, *pr)
+        ops.add(add, b)
+
+    # untimed: OpenMP team start-up and first touch of every page by the team
+    ops.copy(f)
+    ops.apply_q1_gate(f, u2, 0)
+    ops.apply_q1_gate(b, u2, 0)
+    for key, fn, items in (("q1", q1, q1_pos), ("q2", q2, q2_pairs), ("diag", diag, diag_pairs),
+                           ("dens1", dens1, dens1_pos), ("dens2", dens2, dens2_pairs)):
+        if items:
+            out[key] = float(np.mean([timed(lambda x=x: fn(x)) for x in items]))
+    return out
+
+
+def cpu_baseline(args, n):
+    """The reference's algorithm on the host cores (oracle/cpu_ref.c: its CUDA kernels'
+    index rules in C/OpenMP, driven in circuit.rs's order: unfused, one kernel per step, a new
+    state per density injection).  Per gate kind, the fwd + bwd cost is timed on full-size
+    states at sampled positions, and projected onto the workload's gate mix:
+      C2 (the headline workload, n = 28 f32): 560 q1 + 540 q2 gates + 28 q1 densities per step,
+        at all threads (OMP default) and at 1 thread (fewer samples);
+      C3 (example_vqse_ising.py, n = 26 f64): 26 layers x (26 diagonal + 26 q1) + 26 q2
+        densities per loss + gradient call, at all threads.
+    value = C2 gate applications per second (fwd + bwd) at all threads."""
+    # idle OpenMP threads sleep instead of spinning: spinning teams were starved on shared
+    # hosts (64-100 ms for a 2 ms kernel in this container); read when libgomp loads
+    os.environ.setdefault("OMP_WAIT_POLICY", "passive")
+    from oracle.cref import CRefOps
+    from quantum_differentiable_circuit import workloads as W
+    ins, _ = W.layered_circuit(n, args.layers, args.seed)
+    n_q1 = sum(1 for k, _ in ins if k == 8)
+    n_q2 = sum(1 for k, _ in ins if k == 1)
+    n_d1 = sum(1 for k, _ in ins if k == 13)
+    res = {}
+    t_all = time.perf_counter()
+    ops = CRefOps(args.precision)
+    threads = ops.threads()
+    spread = [0, n // 2, n - 1]
+    c2 = _cref_op_costs(ops, n, spread, [(p + 1, p) for p in spread[:-1]] + [(n - 1, n - 2)],
+                        [0, n - 1], [])
+    step = n_q1 * c2["q1"] + n_q2 * c2["q2"] + n_d1 * c2["dens1"]
+    ops.set_threads(1)
+    c2s = _cref_op_costs(ops, n, [n // 2], [(n // 2 + 1, n // 2)], [n // 2], [])
+    ops.set_threads(threads)
+    step1 = n_q1 * c2s["q1"] + n_q2 * c2s["q2"] + n_d1 * c2s["dens1"]
+    res["single_thread"] = {"value": round((n_q1 + n_q2) / step1, 4), "cores": 1,
+                            "s_per_step": round(step1, 2),
+                            "per_gate_s": {k: round(v, 4) for k, v in c2s.items()}}
+    # C3: the VQSE circuit at the example's size, f64
+    n3, layers3 = 26, 26
+    ops64 = CRefOps("f64")
+    c3 = _cref_op_costs(ops64, n3, [0, n3 // 2, n3 - 1], [], [], [(0, 1), (12, 13), (0, n3 - 1)],
+                        [(0, 1), (12, 13), (0, n3 - 1)])
+    call = layers3 * n3 * (c3["diag"] + c3["q1"]) + n3 * c3["dens2"]
+    res["c3_vqse"] = {"s_per_loss_grad_call": round(call, 2), "qubits": n3, "layers": layers3,
+                      "dtype": "c128 (f64)", "cores": ops64.threads(),
+                      "per_gate_s": {k: round(v, 4) for k, v in c3.items()}}
+    wall = time.perf_counter() - t_all
+    return {"value": round((n_q1 + n_q2) / step, 4), "unit": "gate-applications/s (fwd+bwd)",
+            "cores": threads, "kind": "port", "s_per_step": round(step, 2),
+            "per_gate_s": {k: round(v, 4) for k, v in c2.items()},
+            "sample": (f"per-kind fwd+bwd costs of the reference algorithm (oracle/cpu_ref.c, OpenMP, "
+                       f"unfused, circuit.rs order) timed on full n={n} {args.precision} states: q1 at "
+                       f"{len(spread)} positions, q2 at {len(spread)} pairs, q1 density+injection at 2; "
+                       f"projected onto C2's {n_q1} q1 + {n_q2} q2 gates + {n_d1} densities per "
+                       f"step; single_thread: one position per kind; c3_vqse: n=26 f64 diagonal, "
+                       f"q1 and q2-density costs projected onto 26 layers; {wall:.0f} s of CPU time"),
+            **res}
 
 
 def gate_kernel_sample(args, n):
@@ -223,22 +319,88 @@ def dense_gate_sample(args, n):
 
 def vqse_sample(steps=3):
     """Config C3 (example_vqse_ising.py at its own size: n = 26, 26 layers, f64, |+>^n): wall
-    seconds per loss-and-gradient call, the number the example prints (example:133)."""
-    sys.path.insert(0, str(ROOT / "examples"))
-    import vqse_ising
+    seconds per loss-and-gradient call (the number example:133 prints), and the HBM roofline and
+    f64 VALU rate of the call's dominant kernel (HIP events on the circuit's stream)."""
+    from qdc import AutoGradCircuit
     from quantum_differentiable_circuit import workloads as W
     n, layers = 26, 26
-    f = vqse_ising.build(n, layers, "f64")
+    ac = AutoGradCircuit(n, precision="f64")
+    ac.set_state_from_vector(np.ones(1 << n, dtype=ac.dtype) / np.sqrt(1 << n))
+    for kind, pos in W.vqse_ising(n, layers):
+        if kind == W.VAR_Q2_DIAG:
+            ac.add_q2_var_gate_diag(*pos)
+        elif kind == W.VAR_Q1:
+            ac.add_q1_var_gate(*pos)
+        else:
+            ac.get_q2_dens_op_with_grad(*pos)
+    _, fwd_circ = ac.build()
+
+    def f(gates):
+        return fwd_circ.vjp(gates, [])
+
     h = W.tfim_term(1.0)
     p = np.random.default_rng(42).normal(size=2 * layers)
     W.vqse_loss_and_grad(f, p, n, h)  # warm-up
+    ac.circuit.profile(True)
     t0 = time.perf_counter()
     for _ in range(steps):
         e, _ = W.vqse_loss_and_grad(f, p, n, h)
     dt = (time.perf_counter() - t0) / steps
-    return {"s_per_loss_grad_call": round(dt, 4), "energy": round(e, 6), "qubits": n,
-            "layers": layers, "gates": 2 * n * layers, "dtype": "c128 (f64)",
-            "calls": steps}
+    stats = ac.circuit.profile_collect()
+    ac.circuit.profile(False)
+    out = {"s_per_loss_grad_call": round(dt, 4), "energy": round(e, 6), "qubits": n,
+           "layers": layers, "gates": 2 * n * layers, "dtype": "c128 (f64)", "calls": steps}
+    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["total_ms"])
+    avg = dom["total_ms"] / dom["launches"]
+    gbs = dom["algo_bytes"] / dom["launches"] / (avg * 1e-3) / 1e9
+    out["device_ms_per_call"] = round(sum(v["total_ms"] for v in stats.values()) / steps, 2)
+    out["roofline"] = {"bound": "hbm", "kernel": dom_name, "achieved": round(gbs, 1),
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                       "avg_launch_ms": round(avg, 4), "launches_per_call": dom["launches"] // steps,
+                       "algo_bytes_per_launch": dom["algo_bytes"] / dom["launches"]}
+    if dom.get("algo_flops"):
+        tf = dom["algo_flops"] / dom["launches"] / (avg * 1e-3) / 1e12
+        out["compute"] = {"bound": "valu", "kernel": dom_name, "achieved": round(tf, 2),
+                          "peak": VALU_PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
+                          "frac": round(tf / VALU_PEAK_TFLOPS["f64"], 4)}
+    out["kernels"] = {k: {"launches": v["launches"] // steps,
+                          "avg_ms": round(v["total_ms"] / v["launches"], 4)}
+                      for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"])}
+    return out
+
+
+def abi_unfused_sample(args, n):
+    """The same C2 step through the 18-function C ABI in the reference's own call sequence
+    (quantum_differentiable_circuit.abi_circuit.AbiCircuit, circuit.rs:164-429 over
+    QuantizedTensor): what a Rust host linking libqdc per INTEGRATION.md §1 gets.  One step
+    (forward + backward), wall time; every gradient is a host sync as in the reference."""
+    from quantum_differentiable_circuit import workloads as W
+    from quantum_differentiable_circuit.abi_circuit import AbiCircuit
+    ins, var = W.layered_circuit(n, args.layers, args.seed)
+    a = AbiCircuit(n, args.precision)
+    for kind, pos in ins:
+        a.add(kind, *pos)
+    dt = a.dtype
+    vg = [np.ascontiguousarray(g, dtype=dt) for g in var]
+    warm = AbiCircuit(n, args.precision)  # every kernel variant once
+    wins, wvar = W.layered_circuit(n, 1, args.seed)
+    for kind, pos in wins:
+        warm.add(kind, *pos)
+    wd = warm.forward([], [np.ascontiguousarray(g, dtype=dt) for g in wvar])
+    warm.backward(sigma_z_cotangents(len(wd), dt), [], [np.ascontiguousarray(g, dtype=dt) for g in wvar])
+    del warm
+    t0 = time.perf_counter()
+    d = a.forward([], vg)
+    g = a.backward(sigma_z_cotangents(len(d), dt), [], vg)
+    a.state.get_cpu_state_copy() if n <= 20 else None
+    from quantum_differentiable_circuit import primitives_sync
+    primitives_sync(args.precision)
+    el = time.perf_counter() - t0
+    assert all(np.isfinite(x).all() for x in g)
+    return {"value": round(len(vg) / el, 3), "unit": "gate-applications/s (fwd+bwd)",
+            "s_per_step": round(el, 3), "gates": len(vg), "densities": len(d),
+            "path": "AbiCircuit: circuit.rs over the 18 primitives (unfused, one kernel per step, "
+                    "host sync per gradient, a new state per density injection)"}
 
 
 def micro(args):
@@ -252,22 +414,30 @@ def micro(args):
     rows = []
 
     def run(label, setup):
+        """the median over 20 fwd+bwd iterations (after 3 warm-ups) of each
+        kernel's per-launch HIP-event time in the iteration."""
         c = q.circuit_class(prec)(n)
         var = setup(c)
-        c.forward([], var)  # warm-up
-        c.backward(sigma_z_cotangents(1, dt), [], var)
-        c.profile(True)
+        cots = sigma_z_cotangents(1, dt)
         for _ in range(3):
             c.forward([], var)
-            c.backward(sigma_z_cotangents(1, dt), [], var)
-        stats = c.profile_collect()
+            c.backward(cots, [], var)
+        per = {}
+        for _ in range(20):
+            c.profile(True)
+            c.forward([], var)
+            c.backward(cots, [], var)
+            for k, s in c.profile_collect().items():
+                if s["total_ms"] > 0 and k not in ("finalize",):
+                    per.setdefault(k, []).append((s["total_ms"] / s["launches"], s["algo_bytes"] / s["launches"],
+                                                  s["launches"]))
         c.profile(False)
-        for k, s in stats.items():
-            if s["total_ms"] > 0 and k not in ("finalize",):
-                gbs = s["algo_bytes"] / (s["total_ms"] * 1e-3) / 1e9
-                rows.append((label, k, s["launches"], s["total_ms"] / s["launches"], gbs))
-                print(f"{label:14s} {k:18s} n={s['launches']:4d} {s['total_ms'] / s['launches']:8.3f} ms"
-                      f" {gbs:8.1f} GB/s  {gbs / HBM_PEAK_GBS:6.1%}", flush=True)
+        for k, v in per.items():
+            ms = float(np.median([x[0] for x in v]))
+            gbs = v[0][1] / (ms * 1e-3) / 1e9
+            rows.append((label, k, v[0][2], ms, gbs))
+            print(f"{label:14s} {k:18s} n={v[0][2]:4d} {ms:8.3f} ms {gbs:8.1f} GB/s  "
+                  f"{gbs / HBM_PEAK_GBS:6.1%}  (median of {len(v)})", flush=True)
         del c
 
     reps = 8
@@ -354,13 +524,23 @@ def main():
     dom_flops = dom.get("algo_flops", 0.0) / dom["launches"]
     valu_peak = VALU_PEAK_TFLOPS[args.precision]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM bytes per launch from the PMC passes (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py),
+    # quoted only when they were collected on this very library build
+    traffic, traffic_src = None, None
     pmc_path = Path(args.pmc) if args.pmc else ROOT / "profiles" / "pmc_traffic.json"
     if pmc_path.exists():
         try:
-            traffic = json.loads(pmc_path.read_text()).get(dom_name)
-        except Exception:  # noqa: BLE001
-            traffic = None
+            import hashlib
+            pmc = json.loads(pmc_path.read_text())
+            lib = Path(__import__("quantum_differentiable_circuit._native", fromlist=["x"]).lib_path(
+                args.precision))
+            sha = hashlib.sha256(lib.read_bytes()).hexdigest()[:16]
+            if args.precision == "f32" and pmc.get("lib_sha16") == sha:
+                traffic, traffic_src = pmc.get(dom_name), f"{pmc_path.name} (build {sha})"
+            else:
+                traffic_src = f"{pmc_path.name} is from another build ({pmc.get('lib_sha16')} != {sha})"
+        except Exception as e:  # noqa: BLE001
+            traffic_src = f"unreadable: {e}"[:200]
     kernels = {k: {"launches": v["launches"], "avg_ms": round(v["total_ms"] / v["launches"], 4),
                    "GB/s": round(v["algo_bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)
                    if v["total_ms"] > 0 else None,
@@ -381,7 +561,7 @@ def main():
     eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / max(world, 1)
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
-    gate_kernels = dense_kernels = vqse = None
+    gate_kernels = dense_kernels = vqse = abi = None
     if rank == 0 and world == 1 and not args.no_gate_sample:
         # auxiliary samples: a failure there is reported in the line, never loses the headline
         def aux(fn, *a):
@@ -392,6 +572,7 @@ def main():
         gate_kernels = aux(gate_kernel_sample, args, n)
         dense_kernels = aux(dense_gate_sample, args, n)
         vqse = aux(vqse_sample)
+        abi = aux(abi_unfused_sample, args, n)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -427,6 +608,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algo_bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(avg_ms, 4)},
             # fused passes are VALU-bound: their FLOP rate against the vector peak
@@ -441,6 +623,7 @@ def main():
             "gate_kernels": gate_kernels,
             "dense_gate_kernels": dense_kernels,
             "vqse_c3": vqse,
+            "abi_unfused": abi,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

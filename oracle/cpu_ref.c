@@ -234,3 +234,6 @@ EXPORT int cref_threads(void) {
   }
   return t;
 }
+
+/* thread count of the following calls (bench.py times the baseline at 1 thread and at all) */
+EXPORT void cref_set_threads(int t) { omp_set_num_threads(t > 0 ? t : 1); }

@@ -35,6 +35,8 @@ def _lib(precision):
             fn.restype = None
             fn.argtypes = args
         lib.cref_threads.restype = C.c_int
+        lib.cref_set_threads.restype = None
+        lib.cref_set_threads.argtypes = [C.c_int]
         _LIBS[precision] = lib
     return _LIBS[precision]
 
@@ -50,6 +52,9 @@ class CRefOps:
 
     def threads(self):
         return int(self.lib.cref_threads())
+
+    def set_threads(self, t):
+        self.lib.cref_set_threads(int(t))
 
     def _n(self, s):
         return s.size.bit_length() - 1

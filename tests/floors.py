@@ -21,7 +21,7 @@ from oracle import oracle as O
 from oracle.cref import CRefOps
 
 RATIO = 4.0
-ATOL = {"f32": 2.4e-7, "f64": 4.5e-16}
+ATOL = {"f32": 2.4e-7, "f64": 1e-15}
 DT = {"f32": np.complex64, "f64": np.complex128}
 
 

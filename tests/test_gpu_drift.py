@@ -43,7 +43,8 @@ def test_c5_depth_10k_gates_vs_oracle(prec):
     c = build(prec, n, ins)
     fl.check("forward", c.forward([], fl.var), f"C5 n={n} 10k {prec} ")
     fl.check("state", c.get_state(0), f"C5 n={n} 10k {prec} ")
-    fl.check("grads", c.backward(fl.cots, [], fl.var), f"C5 n={n} 10k {prec} ")
+    g = c.backward(fl.cots, [], fl.var)
+    fl.check("grads", g, f"C5 n={n} 10k {prec} ")
     psi = c.get_state(0)
     fl.check("uncomputed", psi, f"C5 n={n} 10k {prec} ")
     fl.check("bwd", c.get_state(2), f"C5 n={n} 10k {prec} ")
@@ -51,8 +52,8 @@ def test_c5_depth_10k_gates_vs_oracle(prec):
     e0[0] = 1
     print(f"[drift] C5 n={n} 10k {prec}: |psi after backward - psi0| = "
           f"{np.linalg.norm(psi.astype(np.complex128) - e0):.3e}")
-    if prec == "f64":
-        assert F.normrel(c.backward(fl.cots, [], fl.var), fl.exact["grads"]) <= 1e-10
+    if prec == "f64":  # f64 at depth within 1e-10 (measured: ~4e-15)
+        assert F.normrel(g, fl.exact["grads"]) <= 1e-10
 
 
 def _stream_uncompute_error(c, n, chunk=1 << 26):
@@ -103,7 +104,7 @@ def test_c5_full_size_10k_gates():
         return sum(np.real(np.trace(x.astype(np.complex128) @ np.diag([1.0, -1.0])))
                    for x in c.forward([], gates))
 
-    eps = 1e-2
+    eps = 1e-3  # |eps p| ~ 0.02 over the 48 gates: curvature error ~2e-3, f32 noise ~4e-3
     lp = loss([(x + eps * y).astype(np.complex64) for x, y in zip(vg, p)])
     lm = loss([(x - eps * y).astype(np.complex64) for x, y in zip(vg, p)])
     fd = (lp - lm) / (2 * eps)
@@ -111,7 +112,7 @@ def test_c5_full_size_10k_gates():
     scale = np.linalg.norm(np.concatenate([g[i] for i in chosen])) * np.linalg.norm(
         np.concatenate([p[i].reshape(-1) for i in chosen]))
     print(f"[fd] C5 n={n}: finite difference {fd:.6e}, analytic {an:.6e}, scale {scale:.3e}")
-    assert abs(fd - an) <= 2e-3 * scale, (fd, an, scale)
+    assert abs(fd - an) <= 1e-3 * scale, (fd, an, scale)
     del c
     gc.collect()
 

@@ -10,6 +10,7 @@ FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
 usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round>
 """
 import csv
+import hashlib
 import json
 import re
 import shutil
@@ -57,6 +58,15 @@ def per_launch(path, counter):
     return {k: sums[k] / counts[k] for k in sums}, dict(counts)
 
 
+LIB = Path(__file__).resolve().parent.parent / "differentiable-quantum-circuit-cuda_amd" / "lib"
+
+
+def lib_sha16(precision="f32"):
+    """Identity of the library the counters were collected on (bench.py reports the traffic only
+    for this same build, so a stale profile cannot be quoted after a kernel change)."""
+    return hashlib.sha256((LIB / f"libqdc_{precision}.so").read_bytes()).hexdigest()[:16]
+
+
 def main(src, dst):
     src, dst = Path(src), Path(dst)
     dst.parent.mkdir(parents=True, exist_ok=True)
@@ -69,6 +79,7 @@ def main(src, dst):
                   "launches_fetch_pass": nf.get(k), "launches_write_pass": nw.get(k),
                   "hbm_bytes_per_launch": traffic[k]} for k in traffic}
     (dst.parent / f"{dst.name}_pmc_traffic.json").write_text(json.dumps(detail, indent=1) + "\n")
+    traffic["lib_sha16"] = lib_sha16()
     (dst.parent / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
     stats = src / "trace" / "trace_kernel_stats.csv"
     if stats.exists():
