@@ -59,10 +59,10 @@ def parse():
     return ap.parse_args()
 
 
-def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None):
+def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None, devices=None):
     from quantum_differentiable_circuit import workloads as W  # synthetic C2 workload
     ins, var = W.layered_circuit(n, layers, seed)
-    c = q.circuit_class(precision)(n, comm=comm, local_shards=local_shards)
+    c = q.circuit_class(precision)(n, comm=comm, local_shards=local_shards, devices=devices)
     for kind, pos in ins:
         c._push(kind, *pos)
     dt = c.dtype
@@ -479,16 +479,18 @@ def main():
         return
 
     n = args.qubits
-    comm = None
-    if world > 1:
+    comm = devices = None
+    if world > 1:  # one process per GPU (torchrun): RCCL id through a file, no torch in the product
         from quantum_differentiable_circuit.distributed import Communicator
-        comm = Communicator(args.precision, device=local)
+        comm = Communicator(args.precision, rank=rank, world=world, device=local)
+    elif args.gpus > 1:  # one plain process driving every GPU (ncclCommInitAll)
+        devices = list(range(args.gpus))
     c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision, comm,
-                               args.local_shards)
+                               args.local_shards, devices)
     ngates = len(vg)
     cots = sigma_z_cotangents(sum(1 for k, _ in ins if k in (12, 13)), c.dtype)
     remaps = 0
-    shards = world if world > 1 else (args.local_shards or 1)
+    shards = world if world > 1 else (len(devices) if devices else (args.local_shards or 1))
     if shards > 1:
         instr = [(k, *p) for k, p in ins]
         f_ops, end = q.plan(n, shards, instr, 1, precision=args.precision)
@@ -558,7 +560,8 @@ def main():
     # the fused path against the per-gate roofline: every gate costs 2S forward and 4S in the
     # reverse sweep (SURVEY.md §8 d) if applied one HBM pass at a time
     state_bytes = (1 << n) * (8 if args.precision == "f32" else 16)
-    eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / max(world, 1)
+    ngpu = world if world > 1 else (len(devices) if devices else 1)
+    eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / ngpu
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
     gate_kernels = dense_kernels = vqse = abi = None
@@ -587,7 +590,7 @@ def main():
             "metric": "gate-applications/sec (fwd+bwd) at n qubits",
             "value": round(value, 3),
             "unit": "gate-applications/s",
-            "n_gpus": world,
+            "n_gpus": ngpu,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -601,7 +604,10 @@ def main():
                        "qubits": n, "layers": args.layers, "gates_per_step": ngates,
                        "densities_per_step": len(cots), "state_GiB": state_gib,
                        "parallelism": (f"state sharded over {world} GPUs by high qubits, "
-                                       f"RCCL all-to-all remaps") if world > 1 else
+                                       f"RCCL all-to-all remaps, one process per GPU") if world > 1 else
+                                      (f"state sharded over {ngpu} GPUs by high qubits, RCCL "
+                                       f"all-to-all remaps, one process (ncclCommInitAll)")
+                                      if devices else
                                       (f"rehearsal: {shards} shards on one GPU (device copies)"
                                        if shards > 1 else "single GPU"),
                        "remaps_per_step": remaps},

@@ -13,7 +13,8 @@ struct qdc_circuit {
 #define QDC_API extern "C" __attribute__((visibility("default")))
 
 static const char* new_circuit(qdc_circuit** out, size_t n, int world, int rank0, int nlocal,
-                               ncclComm_t comm);
+                               ncclComm_t comm, const std::vector<int>* devices = nullptr,
+                               const std::vector<ncclComm_t>* comms = nullptr);
 
 QDC_API const char* qdc_circuit_new(qdc_circuit** out, size_t qubits_number) {
   return new_circuit(out, qubits_number, 1, 0, 1, nullptr);
@@ -36,11 +37,12 @@ QDC_API const char* qdc_circuit_set_state_from_vector(qdc_circuit* c, const qdc_
   if (len != ((size_t)1 << k.n))
     return qdc::fail("Size of the given state does not match the size of the tensor.");
   const size_t shard = (size_t)1 << k.nl;
-  for (size_t s = 0; s < k.sh.size(); ++s)
+  for (size_t s = 0; s < k.sh.size(); ++s) {
+    QDC_TRY(k.sh[s].c().use());
     QDC_HIP(hipMemcpyAsync(k.sh[s].initial, vec + (size_t)(k.ex.rank0 + s) * shard,
-                           shard * sizeof(qdc_complex), hipMemcpyHostToDevice, k.ctx.stream));
-  QDC_HIP(hipStreamSynchronize(k.ctx.stream));
-  return nullptr;
+                           shard * sizeof(qdc_complex), hipMemcpyHostToDevice, k.sh[s].c().stream));
+  }
+  return k.sync_all();
 }
 
 QDC_API const char* qdc_circuit_push(qdc_circuit* c, int kind, size_t pos2, size_t pos1) {
@@ -82,9 +84,11 @@ QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
   const qdc::Shard& s = k.sh[shard];
   const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
   if (!src) return qdc::fail("state %d is not allocated", which);
+  QDC_TRY(k.sync_all());  // every shard's work, not only this shard's stream
+  QDC_TRY(s.c().use());
   QDC_HIP(hipMemcpyAsync(host, src, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
-                         k.ctx.stream));
-  QDC_HIP(hipStreamSynchronize(k.ctx.stream));
+                         s.c().stream));
+  QDC_HIP(hipStreamSynchronize(s.c().stream));
   return nullptr;
 }
 
@@ -99,9 +103,11 @@ QDC_API const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, 
   const qdc::Shard& s = k.sh[shard];
   const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
   if (!src) return qdc::fail("state %d is not allocated", which);
+  QDC_TRY(k.sync_all());
+  QDC_TRY(s.c().use());
   QDC_HIP(hipMemcpyAsync(host, src + offset, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
-                         k.ctx.stream));
-  QDC_HIP(hipStreamSynchronize(k.ctx.stream));
+                         s.c().stream));
+  QDC_HIP(hipStreamSynchronize(s.c().stream));
   return nullptr;
 }
 
@@ -187,11 +193,12 @@ QDC_API void qdc_comm_free(qdc_comm* c) {
 }
 
 static const char* new_circuit(qdc_circuit** out, size_t n, int world, int rank0, int nlocal,
-                               ncclComm_t comm) {
+                               ncclComm_t comm, const std::vector<int>* devices,
+                               const std::vector<ncclComm_t>* comms) {
   *out = nullptr;
   QDC_TRY(qdc::check_n(n));
   qdc_circuit* c = new qdc_circuit();
-  const char* e = c->impl.init((uint32_t)n, world, rank0, nlocal, comm);
+  const char* e = c->impl.init((uint32_t)n, world, rank0, nlocal, comm, devices, comms);
   if (e) {
     c->impl.destroy();
     delete c;
@@ -209,6 +216,45 @@ QDC_API const char* qdc_circuit_new_sharded(qdc_circuit** out, size_t n, qdc_com
 QDC_API const char* qdc_circuit_new_local_shards(qdc_circuit** out, size_t n, int shards) {
   if (shards < 1) return qdc::fail("shards must be >= 1");
   return new_circuit(out, n, shards, 0, shards, nullptr);
+}
+
+// One process, one shard per listed device (ncclCommInitAll over the node's
+// GPUs, the single-process Python API of example_vqse_ising.py).  Distinct devices: RCCL
+// communicators from ncclCommInitAll, collectives grouped over the shards' streams.  One device
+// repeated: the shards share it, each on its own stream, exchanged by copies ordered with
+// events (the same per-shard stream / context / program plumbing, on one GPU).
+QDC_API const char* qdc_circuit_new_devices(qdc_circuit** out, size_t n, int ndev,
+                                            const int* devices) {
+  *out = nullptr;
+  if (ndev < 1 || !devices) return qdc::fail("no devices");
+  std::vector<int> devs(devices, devices + ndev);
+  bool all_same = true, distinct = true;
+  for (int i = 0; i < ndev; ++i)
+    for (int j = 0; j < i; ++j) {
+      all_same = all_same && devs[i] == devs[j];
+      distinct = distinct && devs[i] != devs[j];
+    }
+  if (!all_same && !distinct)
+    return qdc::fail("devices must be all distinct (RCCL) or all the same (one GPU)");
+  int count = 0;
+  QDC_HIP(hipGetDeviceCount(&count));
+  for (int d : devs)
+    if (d < 0 || d >= count) return qdc::fail("device %d does not exist (%d visible)", d, count);
+  QDC_TRY(qdc::check_n(n));
+  const uint32_t g = qdc::log2_exact((size_t)ndev);
+  if (g == UINT32_MAX || (g > 0 && n < 2 * (size_t)g + 3))
+    return qdc::fail("%d devices cannot shard %zu qubits (a power of two, n >= 2g + 3)", ndev, n);
+  int cur = 0;
+  QDC_HIP(hipGetDevice(&cur));
+  std::vector<ncclComm_t> comms;
+  if (ndev > 1 && distinct) {
+    comms.resize(ndev);
+    QDC_NCCL(ncclCommInitAll(comms.data(), ndev, devs.data()));
+  }
+  // from here the circuit owns the communicators (its destroy() frees them, also on error)
+  const char* e = new_circuit(out, n, ndev, 0, ndev, nullptr, &devs, &comms);
+  (void)hipSetDevice(cur);
+  return e;
 }
 
 // ---- planner -----------------------------------------------------------------------------
@@ -236,23 +282,25 @@ QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned
   return plan.size();
 }
 
-QDC_API const char* qdc_circuit_sync(qdc_circuit* c) {
-  QDC_HIP(hipStreamSynchronize(c->impl.ctx.stream));
-  return nullptr;
-}
+QDC_API const char* qdc_circuit_sync(qdc_circuit* c) { return c->impl.sync_all(); }
 
 QDC_API const char* qdc_circuit_profile(qdc_circuit* c, int on) {
-  qdc::Ctx& x = c->impl.ctx;
-  if (on) {
-    QDC_HIP(hipStreamSynchronize(x.stream));
-    x.prof.reset();
+  for (auto& d : c->impl.devs) {
+    qdc::Ctx& x = d->ctx;
+    if (on) {
+      QDC_TRY(x.sync());
+      x.prof.reset();
+    }
+    x.prof.on = on != 0;
   }
-  x.prof.on = on != 0;
   return nullptr;
 }
 
+// launches of every device context (a kernel's count and time summed over the devices)
 QDC_API size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out, size_t cap) {
-  return qdc::prof_collect(c->impl.ctx, out, cap);
+  std::vector<qdc::Ctx*> xs;
+  for (auto& d : c->impl.devs) xs.push_back(&d->ctx);
+  return qdc::prof_collect(xs, out, cap);
 }
 
 QDC_API const char* qdc_build_info(void) {

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -71,53 +72,13 @@ inline const char* check_density_pos(const Instr& in, uint32_t n) {
                          #call, __LINE__, __FILE__, ncclGetErrorString(qdc_r_));          \
   } while (0)
 
-// The shard exchange.  RCCL: one shard per process (one rank per GPU, xGMI); loopback: every
-// shard in this process on the current GPU, exchanged with device-to-device copies.
-struct Exchange {
-  int world = 1;   // total shards
-  int rank0 = 0;   // global index of this process's first shard
-  int nlocal = 1;  // shards held by this process
-  ncclComm_t comm = nullptr;
-
-  // Block j of send[s] (chunk amplitudes) goes to shard j and lands as block s of recv[j].
-  const char* alltoall(Ctx& c, std::vector<cx*>& send, std::vector<cx*>& recv, size_t chunk) {
-    if (world == 1) return nullptr;
-    const double bytes = (double)chunk * sizeof(cx) * (world - 1) * nlocal;
-    hipEvent_t a = nullptr, b = nullptr;
-    if (c.prof.on) {
-      a = c.prof.get();
-      b = c.prof.get();
-      if (a) (void)hipEventRecord(a, c.stream);
-    }
-    if (comm) {
-      QDC_NCCL(ncclAllToAll(send[0], recv[0], chunk * 2, sizeof(real) == 4 ? ncclFloat : ncclDouble,
-                            comm, c.stream));
-    } else {
-      for (int s = 0; s < nlocal; ++s)
-        for (int d = 0; d < nlocal; ++d)
-          QDC_HIP(hipMemcpyAsync(recv[d] + (size_t)s * chunk, send[s] + (size_t)d * chunk,
-                                 chunk * sizeof(cx), hipMemcpyDeviceToDevice, c.stream));
-    }
-    if (c.prof.on && a && b) {
-      (void)hipEventRecord(b, c.stream);
-      c.prof.recs.push_back({"alltoall", bytes, 0.0, a, b});  // link bytes, not HBM bytes
-    }
-    return nullptr;
-  }
-  // in-place sum over all shards of `count` complex values
-  const char* allreduce(Ctx& c, std::vector<cx*>& bufs, size_t count) {
-    if (world == 1 || count == 0) return nullptr;
-    if (comm) {
-      QDC_NCCL(ncclAllReduce(bufs[0], bufs[0], count * 2, sizeof(real) == 4 ? ncclFloat : ncclDouble,
-                             ncclSum, comm, c.stream));
-      return nullptr;
-    }
-    for (int s = 1; s < nlocal; ++s) QDC_TRY(elementwise_count<2>(c, bufs[s], bufs[0], count));
-    for (int s = 1; s < nlocal; ++s)
-      QDC_HIP(hipMemcpyAsync(bufs[s], bufs[0], count * sizeof(cx), hipMemcpyDeviceToDevice,
-                             c.stream));
-    return nullptr;
-  }
+// Per-device resources of a circuit: a context (stream, reduction arena, profiling) and the
+// device copy of the fused-pass program.  One per shard when the shards run on their own
+// streams (single-process multi-GPU, or the multi-stream rehearsal on one GPU), else one shared
+// by every local shard.
+struct DevRes {
+  Ctx ctx;
+  unsigned char* prog_dev = nullptr;
 };
 
 struct Shard {
@@ -127,13 +88,126 @@ struct Shard {
   cx* scratch = nullptr;  // all-to-all staging (allocated when world > 1)
   cx* dens = nullptr;
   cx* grads = nullptr;
+  DevRes* d = nullptr;  // the shard's device resources
+  Ctx& c() const { return d->ctx; }
+};
+
+// The shard exchange.  Transports:
+//   * RCCL, one shard per process (one rank per GPU, xGMI): `comm`;
+//   * RCCL, every shard of the job in this process, one per GPU (ncclCommInitAll): `comms`,
+//     one collective per shard inside ncclGroupStart/End, each on its shard's stream;
+//   * loopback, every shard on this process's one GPU: device-to-device copies — on one shared
+//     stream, or (`multi_stream`) on the shards' own streams ordered by events.
+struct Exchange {
+  int world = 1;   // total shards
+  int rank0 = 0;   // global index of this process's first shard
+  int nlocal = 1;  // shards held by this process
+  ncclComm_t comm = nullptr;
+  std::vector<ncclComm_t> comms;
+  bool multi_stream = false;
+  std::vector<hipEvent_t> ev;  // multi_stream: one per shard
+
+  static ncclDataType_t type() { return sizeof(real) == 4 ? ncclFloat : ncclDouble; }
+  const char* events(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e;
+      QDC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+    return nullptr;
+  }
+  // every shard stream waits for every other shard stream's work so far
+  const char* join(std::vector<Shard>& sh) {
+    QDC_TRY(events(sh.size()));
+    for (size_t s = 0; s < sh.size(); ++s) {
+      QDC_TRY(sh[s].c().use());
+      QDC_HIP(hipEventRecord(ev[s], sh[s].c().stream));
+    }
+    for (size_t d = 0; d < sh.size(); ++d)
+      for (size_t s = 0; s < sh.size(); ++s)
+        if (s != d) QDC_HIP(hipStreamWaitEvent(sh[d].c().stream, ev[s], 0));
+    return nullptr;
+  }
+  void prof_begin(Shard& s, hipEvent_t& a, hipEvent_t& b) {
+    Ctx& c = s.c();
+    a = b = nullptr;
+    if (c.prof.on) {
+      a = c.prof.get();
+      b = c.prof.get();
+      if (a) (void)hipEventRecord(a, c.stream);
+    }
+  }
+  void prof_end(Shard& s, hipEvent_t a, hipEvent_t b, double bytes) {
+    Ctx& c = s.c();
+    if (c.prof.on && a && b) {
+      (void)hipEventRecord(b, c.stream);
+      c.prof.recs.push_back({"alltoall", bytes, 0.0, a, b});  // link bytes, not HBM bytes
+    }
+  }
+
+  // Block j of send[s] (chunk amplitudes) goes to shard j and lands as block s of recv[j].
+  const char* alltoall(std::vector<Shard>& sh, std::vector<cx*>& send, std::vector<cx*>& recv,
+                       size_t chunk) {
+    if (world == 1) return nullptr;
+    const double bytes = (double)chunk * sizeof(cx) * (world - 1);  // per shard
+    std::vector<hipEvent_t> pa(sh.size()), pb(sh.size());
+    for (size_t s = 0; s < sh.size(); ++s) prof_begin(sh[s], pa[s], pb[s]);
+    if (comm) {
+      QDC_NCCL(ncclAllToAll(send[0], recv[0], chunk * 2, type(), comm, sh[0].c().stream));
+    } else if (!comms.empty()) {
+      QDC_NCCL(ncclGroupStart());
+      for (size_t s = 0; s < sh.size(); ++s)
+        QDC_NCCL(ncclAllToAll(send[s], recv[s], chunk * 2, type(), comms[s], sh[s].c().stream));
+      QDC_NCCL(ncclGroupEnd());
+    } else {
+      if (multi_stream) QDC_TRY(join(sh));  // sources written, destinations free
+      for (int d = 0; d < nlocal; ++d)
+        for (int s = 0; s < nlocal; ++s)
+          QDC_HIP(hipMemcpyAsync(recv[d] + (size_t)s * chunk, send[s] + (size_t)d * chunk,
+                                 chunk * sizeof(cx), hipMemcpyDeviceToDevice, sh[d].c().stream));
+      if (multi_stream) QDC_TRY(join(sh));  // no source is rewritten before every copy is done
+    }
+    for (size_t s = 0; s < sh.size(); ++s) prof_end(sh[s], pa[s], pb[s], bytes);
+    return nullptr;
+  }
+  // in-place sum over all shards of `count` complex values (every shard's buffer holds the sum)
+  const char* allreduce(std::vector<Shard>& sh, std::vector<cx*>& bufs, size_t count) {
+    if (world == 1 || count == 0) return nullptr;
+    if (comm) {
+      QDC_NCCL(ncclAllReduce(bufs[0], bufs[0], count * 2, type(), ncclSum, comm, sh[0].c().stream));
+      return nullptr;
+    }
+    if (!comms.empty()) {
+      QDC_NCCL(ncclGroupStart());
+      for (size_t s = 0; s < sh.size(); ++s)
+        QDC_NCCL(ncclAllReduce(bufs[s], bufs[s], count * 2, type(), ncclSum, comms[s],
+                               sh[s].c().stream));
+      QDC_NCCL(ncclGroupEnd());
+      return nullptr;
+    }
+    if (multi_stream) QDC_TRY(join(sh));
+    Ctx& c0 = sh[0].c();
+    QDC_TRY(c0.use());
+    for (int s = 1; s < nlocal; ++s) QDC_TRY(elementwise_count<2>(c0, bufs[s], bufs[0], count));
+    for (int s = 1; s < nlocal; ++s)
+      QDC_HIP(hipMemcpyAsync(bufs[s], bufs[0], count * sizeof(cx), hipMemcpyDeviceToDevice,
+                             c0.stream));
+    if (multi_stream) QDC_TRY(join(sh));
+    return nullptr;
+  }
+  void destroy() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    for (auto c : comms) (void)ncclCommDestroy(c);
+    comms.clear();
+  }
 };
 
 struct Circuit {
   uint32_t n = 0;   // logical qubits
   uint32_t g = 0;   // rank bits
   uint32_t nl = 0;  // local qubits of a shard
-  Ctx ctx;
+  std::vector<std::unique_ptr<DevRes>> devs;  // per-device resources (sh[s].d points here)
   Exchange ex;
   std::vector<Shard> sh;
   QubitMap layout;  // physical layout of every shard's `state` (identity until a remap)
@@ -159,14 +233,30 @@ struct Circuit {
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
   uint32_t last_fused_grid = 0;
-  unsigned char* prog_dev = nullptr;   // fop descriptors + gate matrices of one pass
-  unsigned char* prog_host = nullptr;  // pinned staging
+  unsigned char* prog_host = nullptr;  // pinned staging of the pass program (every device's copy)
   std::vector<StagePost> stage_post;   // gradient recipes of the last backward's stages
   size_t prog_cap = 0;
 
-  // world = total shards (power of two), nlocal = shards in this process
+  Ctx& ctx0() { return devs[0]->ctx; }
+  const char* sync_all() {
+    for (auto& d : devs) QDC_TRY(d->ctx.sync());
+    return nullptr;
+  }
+  const char* flush_all() {  // pending reduction slots of every context
+    for (auto& d : devs) {
+      QDC_TRY(d->ctx.use());
+      QDC_TRY(d->ctx.flush());
+    }
+    return nullptr;
+  }
+
+  // world = total shards (power of two), nlocal = shards in this process.  devices: one device
+  // per local shard, each shard on its own stream (nullptr: every local shard on the current
+  // device and one stream).  comms: one RCCL communicator per local shard (ncclCommInitAll;
+  // devices then distinct), or none (copies between the streams of one device).
   const char* init(uint32_t qubits, int world = 1, int rank0 = 0, int nlocal = 1,
-                   ncclComm_t comm = nullptr) {
+                   ncclComm_t comm = nullptr, const std::vector<int>* devices = nullptr,
+                   const std::vector<ncclComm_t>* comms = nullptr) {
     n = qubits;
     const uint32_t gg = log2_exact((size_t)world);
     if (gg == UINT32_MAX || gg > 8) return fail("the number of shards must be a power of two <= 256");
@@ -178,6 +268,8 @@ struct Circuit {
     ex.rank0 = rank0;
     ex.nlocal = nlocal;
     ex.comm = comm;
+    if (comms) ex.comms = *comms;
+    ex.multi_stream = devices != nullptr && ex.comms.empty() && nlocal > 1;
     layout.identity(n, g);
     if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
@@ -196,44 +288,61 @@ struct Circuit {
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
       fused_blocks = (uint32_t)std::max(1, std::min(atoi(e), (int)NBMAX));
-    int dev = 0;
-    QDC_HIP(hipGetDevice(&dev));
-    QDC_TRY(ctx.init(dev));
+    int cur = 0;
+    QDC_HIP(hipGetDevice(&cur));
+    const int ndev = devices ? nlocal : 1;
+    for (int i = 0; i < ndev; ++i) {
+      devs.push_back(std::make_unique<DevRes>());
+      QDC_TRY(devs.back()->ctx.init(devices ? (*devices)[i] : cur));
+    }
     const size_t bytes = ((size_t)1 << nl) * sizeof(cx);
     sh.resize(nlocal);
     for (int s = 0; s < nlocal; ++s) {
+      sh[s].d = devs[devices ? s : 0].get();
+      Ctx& c = sh[s].c();
+      QDC_TRY(c.use());
       QDC_HIP(hipMalloc(&sh[s].initial, bytes));
       QDC_HIP(hipMalloc(&sh[s].state, bytes));
       if (g > 0) QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
       // QuantizedTensor::new_standard + clone (circuit.rs:96-102): |0..0> lives on shard 0
       if (rank0 + s == 0)
-        QDC_TRY(set_standard(ctx, sh[s].initial, nl));
+        QDC_TRY(set_standard(c, sh[s].initial, nl));
       else
-        QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, ctx.stream));
-      QDC_TRY(elementwise<0>(ctx, sh[s].initial, sh[s].state, nl));
+        QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, c.stream));
+      QDC_TRY(elementwise<0>(c, sh[s].initial, sh[s].state, nl));
     }
-    QDC_HIP(hipStreamSynchronize(ctx.stream));
+    QDC_TRY(sync_all());
+    QDC_HIP(hipSetDevice(cur));
     return nullptr;
   }
   void destroy() {
-    if (ctx.stream) (void)hipStreamSynchronize(ctx.stream);
-    for (auto& s : sh)
+    (void)sync_all();
+    for (auto& s : sh) {
+      if (s.d) (void)s.d->ctx.use();
       for (cx* p : {s.initial, s.state, s.bwd, s.scratch, s.dens, s.grads})
         if (p) (void)hipFree(p);
+    }
     sh.clear();
     if (host_out) (void)hipHostFree(host_out);
     host_out = nullptr;
-    if (prog_dev) (void)hipFree(prog_dev);
+    for (auto& d : devs) {
+      (void)d->ctx.use();
+      if (d->prog_dev) (void)hipFree(d->prog_dev);
+      d->prog_dev = nullptr;
+      d->ctx.destroy();
+    }
+    devs.clear();
     if (prog_host) (void)hipHostFree(prog_host);
-    prog_dev = prog_host = nullptr;
-    ctx.destroy();
+    prog_host = nullptr;
+    ex.destroy();
   }
 
   const char* ensure_out(bool dens, size_t count) {
     size_t& cap = dens ? dens_cap : grads_cap;
     if (count <= cap) return nullptr;
-    QDC_HIP(hipStreamSynchronize(ctx.stream));
+    QDC_TRY(sync_all());
     for (auto& s : sh) {
+      QDC_TRY(s.c().use());
       cx*& p = dens ? s.dens : s.grads;
       if (p) QDC_HIP(hipFree(p));
       p = nullptr;
@@ -245,7 +354,7 @@ struct Circuit {
   const char* ensure_host(size_t count) {
     if (count <= host_cap) return nullptr;
     if (host_out) {
-      QDC_HIP(hipStreamSynchronize(ctx.stream));
+      QDC_TRY(sync_all());
       QDC_HIP(hipHostFree(host_out));
     }
     host_out = nullptr;
@@ -354,7 +463,8 @@ struct Circuit {
       for (size_t s = 0; s < sh.size(); ++s) {
         cx*& buf = which == 0 ? sh[s].state : sh[s].bwd;
         if (r.pack) {
-          QDC_TRY(pack(ctx, buf, sh[s].scratch, r.victims, g, nl));
+          QDC_TRY(sh[s].c().use());
+          QDC_TRY(pack(sh[s].c(), buf, sh[s].scratch, r.victims, g, nl));
           send[s] = sh[s].scratch;
           recv[s] = buf;
         } else {
@@ -362,7 +472,7 @@ struct Circuit {
           recv[s] = sh[s].scratch;
         }
       }
-      QDC_TRY(ex.alltoall(ctx, send, recv, chunk));
+      QDC_TRY(ex.alltoall(sh, send, recv, chunk));
       if (!r.pack)
         for (size_t s = 0; s < sh.size(); ++s)
           std::swap(which == 0 ? sh[s].state : sh[s].bwd, sh[s].scratch);
@@ -480,11 +590,15 @@ struct Circuit {
     mats_off = ((nfops * sizeof(fop) + 255) / 256) * 256;
     const size_t bytes = mats_off + (nops * 32 + nfops * 12 + items.size() * 32) * sizeof(cx);  // <= 2 R^2 = 32 per stage
     if (bytes > prog_cap) {
-      QDC_HIP(hipStreamSynchronize(ctx.stream));
-      if (prog_dev) QDC_HIP(hipFree(prog_dev));
+      QDC_TRY(sync_all());
+      for (auto& d : devs) {
+        QDC_TRY(d->ctx.use());
+        if (d->prog_dev) QDC_HIP(hipFree(d->prog_dev));
+        d->prog_dev = nullptr;
+        QDC_HIP(hipMalloc(&d->prog_dev, bytes));
+      }
       if (prog_host) QDC_HIP(hipHostFree(prog_host));
-      prog_dev = prog_host = nullptr;
-      QDC_HIP(hipMalloc(&prog_dev, bytes));
+      prog_host = nullptr;
       QDC_HIP(hipHostMalloc(&prog_host, bytes));
       prog_cap = bytes;
     }
@@ -738,8 +852,11 @@ struct Circuit {
       it.nstage = n;
       if (rq_stats) fprintf(stderr, "rq pass: %zu stages, %u ops (T=%u lc=%u)\n", pf.size(), n, it.tbits, it.lc);
     }
-    QDC_HIP(hipMemcpyAsync(prog_dev, prog_host, mats_off + mo * sizeof(cx),
-                           hipMemcpyHostToDevice, ctx.stream));
+    for (auto& d : devs) {  // prog_host is not rewritten before the call's final sync
+      QDC_TRY(d->ctx.use());
+      QDC_HIP(hipMemcpyAsync(d->prog_dev, prog_host, mats_off + mo * sizeof(cx),
+                             hipMemcpyHostToDevice, d->ctx.stream));
+    }
     return nullptr;
   }
 
@@ -751,8 +868,9 @@ struct Circuit {
     return k_fused<TWO, TB, HASRED, WF, NT>;
   }
   template <bool TWO, bool HASRED, bool WF>
-  const char* launch_fused(const char* name, double bytes, const fgeo& fg, chunk* f, chunk* b,
-                           const fop* fops, const cx* mats, cx* partials, uint64_t stride) {
+  const char* launch_fused(Ctx& ctx, const char* name, double bytes, const fgeo& fg, chunk* f,
+                           chunk* b, const fop* fops, const cx* mats, cx* partials,
+                           uint64_t stride) {
     // 256 threads per tile (measured: 128 threads with twice the quartets per thread and
     // occupancy 2 was 2-4 % slower)
     constexpr int NT = 256;
@@ -769,9 +887,9 @@ struct Circuit {
                             f, b, fops, mats, g, partials, stride);
   }
   // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
-  const char* launch_rq(const char* name, double bytes, const fgeo& fg, bool two, uint32_t tbits,
-                        uint32_t l0, chunk* f, chunk* b, const fop* fops, const cx* mats,
-                        cx* partials, uint64_t stride) {
+  const char* launch_rq(Ctx& ctx, const char* name, double bytes, const fgeo& fg, bool two,
+                        uint32_t tbits, uint32_t l0, chunk* f, chunk* b, const fop* fops,
+                        const cx* mats, cx* partials, uint64_t stride) {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     const void* kern = nullptr;
@@ -804,7 +922,7 @@ struct Circuit {
 #undef QDC_RQ_LAUNCH
     return fail("no register-resident kernel launched");
 #else
-    (void)name; (void)bytes; (void)fg; (void)two; (void)tbits; (void)l0; (void)f; (void)b;
+    (void)ctx; (void)name; (void)bytes; (void)fg; (void)two; (void)tbits; (void)l0; (void)f; (void)b;
     (void)fops; (void)mats; (void)partials; (void)stride;
     return fail("register-resident passes are f32 only");
 #endif
@@ -840,8 +958,7 @@ struct Circuit {
     fg.nops = it.nstage;
     fg.ngrad = it.has_red ? (uint32_t)it.grad_slots.size() : 0;
     fg.ntiles = nchunks_of(nl) >> (it.lc + it.h);
-    const fop* fops = reinterpret_cast<const fop*>(prog_dev + it.fop_off);
-    const cx* mats = reinterpret_cast<const cx*>(prog_dev + mats_off);
+
     // algorithmic bytes: each state read once, written once if the pass changes it
     const double S = state_bytes(nl);
     const double bytes = two ? (it.writes_f ? 4.0 : 3.0) * S : (it.writes_f ? 2.0 : 1.0) * S;
@@ -850,6 +967,10 @@ struct Circuit {
     const char* name = two ? (it.writes_f ? "fused_reverse" : "fused_inject")
                            : (it.writes_f ? "fused_apply" : "fused_density");
     for (auto& s : sh) {
+      Ctx& ctx = s.c();
+      QDC_TRY(ctx.use());
+      const fop* fops = reinterpret_cast<const fop*>(s.d->prog_dev + it.fop_off);
+      const cx* mats = reinterpret_cast<const cx*>(s.d->prog_dev + mats_off);
       chunk* f = reinterpret_cast<chunk*>(s.state);
       chunk* b = reinterpret_cast<chunk*>(s.bwd);
       cx* parts = nullptr;
@@ -864,18 +985,18 @@ struct Circuit {
       const uint64_t stride = (uint64_t)NBMAX * RED;
       ctx.next_flops = flops;
       if (it.rq) {
-        QDC_TRY(launch_rq(name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride));
+        QDC_TRY(launch_rq(ctx, name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride));
       } else if (two) {
         if (it.writes_f)
-          QDC_TRY((launch_fused<true, true, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
+          QDC_TRY((launch_fused<true, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
         else
-          QDC_TRY((launch_fused<true, false, false>(name, bytes, fg, f, b, fops, mats, parts, stride)));
+          QDC_TRY((launch_fused<true, false, false>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else if (!it.has_red) {
-        QDC_TRY((launch_fused<false, false, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
+        QDC_TRY((launch_fused<false, false, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else if (it.writes_f) {
-        QDC_TRY((launch_fused<false, true, true>(name, bytes, fg, f, b, fops, mats, parts, stride)));
+        QDC_TRY((launch_fused<false, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else {
-        QDC_TRY((launch_fused<false, true, false>(name, bytes, fg, f, b, fops, mats, parts, stride)));
+        QDC_TRY((launch_fused<false, true, false>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       }
       if (fg.ngrad > 0)
         for (uint32_t slot : it.grad_slots) ctx.commit(slot, last_fused_grid);
@@ -886,8 +1007,8 @@ struct Circuit {
   }
 
   // --- forward (Circuit::run / Circuit::forward) --------------------------------------------
-  const char* apply_gate(const Instr& in, const qdc_complex* g4, cx* s, uint32_t p2, uint32_t p1,
-                         bool uncompute) {
+  const char* apply_gate(Ctx& ctx, const Instr& in, const qdc_complex* g4, cx* s, uint32_t p2,
+                         uint32_t p1, bool uncompute) {
     if (is_diag(in.kind)) {
       const diag4 d = to_diag(g4);
       return apply_diag(ctx, s, uncompute ? conj_diag(d) : d, p2, p1, nl,
@@ -922,7 +1043,10 @@ struct Circuit {
     QDC_TRY(ensure_out(true, std::max<size_t>(nout, 1) * RED));
     // every pass starts from `initial`, which is always in the identity layout
     layout.identity(n, g);
-    for (auto& s : sh) QDC_TRY(elementwise<0>(ctx, s.initial, s.state, nl));
+    for (auto& s : sh) {
+      QDC_TRY(s.c().use());
+      QDC_TRY(elementwise<0>(s.c(), s.initial, s.state, nl));
+    }
     std::vector<uint32_t> out_idx(ins.size(), 0);
     {
       uint32_t o = 0;
@@ -951,9 +1075,11 @@ struct Circuit {
       }
       const Instr& in = ins[op.instr];
       for (auto& s : sh) {
+        Ctx& ctx = s.c();
+        QDC_TRY(ctx.use());
         if (is_const(in.kind) || is_var(in.kind)) {
           const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
-          QDC_TRY(apply_gate(in, g4, s.state, op.pos2, op.pos1, false));
+          QDC_TRY(apply_gate(ctx, in, g4, s.state, op.pos2, op.pos1, false));
         } else if (is_q1_density(in.kind)) {
           QDC_TRY(density<2>(ctx, s.state, op.pos2, op.pos2, nl, s.dens, out_idx[op.instr], 0));
         } else {
@@ -961,10 +1087,10 @@ struct Circuit {
         }
       }
     }
-    QDC_TRY(ctx.flush());
+    QDC_TRY(flush_all());
     std::vector<cx*> bufs;
     for (auto& s : sh) bufs.push_back(s.dens);
-    QDC_TRY(ex.allreduce(ctx, bufs, nout * RED));
+    QDC_TRY(ex.allreduce(sh, bufs, nout * RED));
     std::vector<int> widths;
     for (auto& in : ins)
       if (is_diff_density(in.kind) || (mode == QDC_MODE_RUN && is_density(in.kind)))
@@ -978,14 +1104,13 @@ struct Circuit {
                       size_t total = 0) {
     const size_t count = widths.size();
     total = std::max(total, count);
-    if (total == 0) {
-      QDC_HIP(hipStreamSynchronize(ctx.stream));
-      return nullptr;
-    }
+    if (total == 0) return sync_all();
     QDC_TRY(ensure_host(total * RED));
+    Ctx& c0 = sh[0].c();
+    QDC_TRY(c0.use());
     QDC_HIP(hipMemcpyAsync(host_out, dev, sizeof(cx) * total * RED, hipMemcpyDeviceToHost,
-                           ctx.stream));
-    QDC_HIP(hipStreamSynchronize(ctx.stream));
+                           c0.stream));
+    QDC_TRY(sync_all());
     size_t w = 0;
     for (size_t j = 0; j < count; ++j) {
       for (int k = 0; k < widths[j]; ++k) {
@@ -1003,13 +1128,18 @@ struct Circuit {
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
     const size_t nvar = n_var();
     for (auto& s : sh)
-      if (!s.bwd) QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
+      if (!s.bwd) {
+        QDC_TRY(s.c().use());
+        QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
+      }
     // slots [0, nvar): per-gate gradients; [nvar, nvar + stages): fused stages' Gamma
     const size_t nslots = std::max<size_t>(2 * nvar, 1);
     QDC_TRY(ensure_out(false, nslots * RED));
     // variable gates met before the first cotangent keep zero gradients (circuit.rs:327-331)
-    for (auto& s : sh)
-      QDC_HIP(hipMemsetAsync(s.grads, 0, sizeof(cx) * nslots * RED, ctx.stream));
+    for (auto& s : sh) {
+      QDC_TRY(s.c().use());
+      QDC_HIP(hipMemsetAsync(s.grads, 0, sizeof(cx) * nslots * RED, s.c().stream));
+    }
     std::vector<uint32_t> var_idx(ins.size(), 0);
     {
       uint32_t v = 0;
@@ -1037,8 +1167,10 @@ struct Circuit {
       if (item.type == 2) {
         const bool two = item.ops[0] >= first_inject;
         if (two && !have_bwd) {  // the first injection is fused: it adds into a zero bwd
-          for (auto& s : sh)
-            QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), ctx.stream));
+          for (auto& s : sh) {
+            QDC_TRY(s.c().use());
+            QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));
+          }
           have_bwd = true;
         }
         QDC_TRY(run_fused(item, two, mats_off, true));
@@ -1054,8 +1186,10 @@ struct Circuit {
         const bool var = is_var(in.kind);
         const qdc_complex* g4 = var ? vg.at(gidx[op.instr]) : cg.at(gidx[op.instr]);
         for (auto& s : sh) {
+          Ctx& ctx = s.c();
+          QDC_TRY(ctx.use());
           if (!have_bwd) {
-            QDC_TRY(apply_gate(in, g4, s.state, op.pos2, op.pos1, true));
+            QDC_TRY(apply_gate(ctx, in, g4, s.state, op.pos2, op.pos1, true));
             continue;
           }
           cx* gbase = var ? s.grads : nullptr;
@@ -1085,6 +1219,8 @@ struct Circuit {
       } else {  // Diff density: inject its cotangent
         const qdc_complex* gd = dg.at(gidx[op.instr]);
         for (auto& s : sh) {
+          Ctx& ctx = s.c();
+          QDC_TRY(ctx.use());
           if (is_q1_density(in.kind))
             QDC_TRY(inject<2>(ctx, s.state, s.bwd, transpose<2>(to_mat<2>(gd)), op.pos2, op.pos2, nl,
                               !have_bwd));
@@ -1095,11 +1231,11 @@ struct Circuit {
         have_bwd = true;
       }
     }
-    QDC_TRY(ctx.flush());
+    QDC_TRY(flush_all());
     const size_t used = nvar + stage_post.size();
     std::vector<cx*> bufs;
     for (auto& s : sh) bufs.push_back(s.grads);
-    QDC_TRY(ex.allreduce(ctx, bufs, used * RED));
+    QDC_TRY(ex.allreduce(sh, bufs, used * RED));
     std::vector<int> widths;
     for (auto& in : ins)
       if (is_var(in.kind)) widths.push_back(gate_len(in.kind));

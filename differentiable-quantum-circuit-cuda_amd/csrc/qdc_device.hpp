@@ -122,8 +122,24 @@ struct Ctx {
     if (red_cap > NBMAX) red_cap = NBMAX;
     return nullptr;
   }
+  // make this context's device current (launches and allocations of a shard go to its device)
+  const char* use() const {
+    int cur = -1;
+    QDC_HIP(hipGetDevice(&cur));
+    if (cur != device) QDC_HIP(hipSetDevice(device));
+    return nullptr;
+  }
+  const char* sync() const {
+    if (!stream) return nullptr;
+    QDC_TRY(use());
+    QDC_HIP(hipStreamSynchronize(stream));
+    return nullptr;
+  }
   void destroy() {
-    if (stream) (void)hipStreamSynchronize(stream);
+    if (stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+    }
     if (partials) (void)hipFree(partials);
     if (results) (void)hipFree(results);
     if (host_results) (void)hipHostFree(host_results);

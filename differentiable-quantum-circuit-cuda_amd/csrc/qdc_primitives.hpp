@@ -61,27 +61,32 @@ inline const char* abi_finish_reduction(Ctx& c, qdc_complex* out, int K) {
 
 // per-kernel sums of a context's profiled launches (qdc_circuit_profile_collect,
 // qdc_abi_profile_collect)
-inline size_t prof_collect(Ctx& x, qdc_kernel_stat* out, size_t cap) {
-  (void)hipStreamSynchronize(x.stream);
+inline size_t prof_collect(const std::vector<Ctx*>& xs, qdc_kernel_stat* out, size_t cap) {
   std::vector<qdc_kernel_stat> agg;
-  for (auto& r : x.prof.recs) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = 0.f;
-    qdc_kernel_stat* s = nullptr;
-    for (auto& a : agg)
-      if (strncmp(a.name, r.name, sizeof(a.name)) == 0) s = &a;
-    if (!s) {
-      agg.push_back({});
-      s = &agg.back();
-      strncpy(s->name, r.name, sizeof(s->name) - 1);
+  for (Ctx* x : xs) {
+    (void)x->sync();
+    for (auto& r : x->prof.recs) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = 0.f;
+      qdc_kernel_stat* s = nullptr;
+      for (auto& a : agg)
+        if (strncmp(a.name, r.name, sizeof(a.name)) == 0) s = &a;
+      if (!s) {
+        agg.push_back({});
+        s = &agg.back();
+        strncpy(s->name, r.name, sizeof(s->name) - 1);
+      }
+      s->launches += 1;
+      s->total_ms += ms;
+      s->algo_bytes += r.bytes;
+      s->algo_flops += r.flops;
     }
-    s->launches += 1;
-    s->total_ms += ms;
-    s->algo_bytes += r.bytes;
-    s->algo_flops += r.flops;
   }
   for (size_t i = 0; i < agg.size() && i < cap; ++i) out[i] = agg[i];
   return agg.size();
+}
+inline size_t prof_collect(Ctx& x, qdc_kernel_stat* out, size_t cap) {
+  return prof_collect(std::vector<Ctx*>{&x}, out, cap);
 }
 
 }  // namespace qdc

@@ -60,10 +60,14 @@ def _flatten(arrays, dtype, what, msg):
 class _CircuitBase:
     _precision = "f32"
 
-    def __init__(self, qubits_number: int, comm=None, local_shards: int | None = None):
-        """`comm` (a `distributed.Communicator`) shards the state over its ranks, one GPU per
-        process; `local_shards=G` keeps G shards on this GPU (same data path, device copies
-        instead of RCCL).  Neither exists in the reference, which is single-GPU."""
+    def __init__(self, qubits_number: int, comm=None, local_shards: int | None = None,
+                 devices=None):
+        """Sharding (none of it exists in the reference, which is single-GPU):
+        `comm` (a `distributed.Communicator`) shards the state over its ranks, one GPU per
+        process; `devices` (a count or a list of device indices) shards it over several GPUs
+        driven by this one process (ncclCommInitAll; a repeated device keeps every shard on it,
+        each on its own stream); `local_shards=G` keeps G shards on this GPU and one stream
+        (same data path, device copies instead of RCCL)."""
         self._lib = load(self._precision)
         self._dtype = np.dtype(PRECISIONS[self._precision])
         h = C.c_void_p()
@@ -71,6 +75,10 @@ class _CircuitBase:
             if comm.precision != self._precision:
                 raise ValueError("communicator was created for the other precision library")
             check(self._lib.qdc_circuit_new_sharded(C.byref(h), int(qubits_number), comm.handle))
+        elif devices is not None:
+            devs = list(range(devices)) if isinstance(devices, int) else [int(d) for d in devices]
+            arr = (C.c_int * len(devs))(*devs)
+            check(self._lib.qdc_circuit_new_devices(C.byref(h), int(qubits_number), len(devs), arr))
         elif local_shards is not None:
             check(self._lib.qdc_circuit_new_local_shards(C.byref(h), int(qubits_number),
                                                          int(local_shards)))

@@ -32,6 +32,7 @@ RUNTIME = (
     "qdc_circuit_backward", "qdc_circuit_get_state", "qdc_circuit_sync", "qdc_circuit_profile",
     "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
     "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
+    "qdc_circuit_new_devices",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
     "qdc_rq_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
 )
@@ -98,6 +99,7 @@ def _proto(lib):
         "qdc_comm_free": (None, [_P]),
         "qdc_circuit_new_sharded": (_E, [C.POINTER(_P), _S, _P]),
         "qdc_circuit_new_local_shards": (_E, [C.POINTER(_P), _S, C.c_int]),
+        "qdc_circuit_new_devices": (_E, [C.POINTER(_P), _S, C.c_int, C.POINTER(C.c_int)]),
         "qdc_circuit_layout": (_E, [_P, C.POINTER(C.c_uint), C.POINTER(C.c_int),
                                     C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "qdc_circuit_get_shard": (_E, [_P, C.c_int, C.c_int, _P, _S]),

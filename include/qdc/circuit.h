@@ -120,8 +120,9 @@ const char* qdc_build_info(void);
  * which logical qubit sits at which physical bit; an op that needs a global qubit is preceded
  * by a REMAP: one all-to-all per state that swaps all g global qubits with g local ones.
  * Densities and gradients are summed over ranks (one all-reduce per call), so every rank
- * returns the full results.  Two transports:
+ * returns the full results.  Transports:
  *   - qdc_circuit_new_sharded: one shard per process, RCCL over xGMI (qdc_comm_*);
+ *   - qdc_circuit_new_devices: one process, one shard per GPU, RCCL (ncclCommInitAll);
  *   - qdc_circuit_new_local_shards: every shard on the current GPU, exchanged with device
  *     copies (the same data path on one GPU; used by the single-GPU parity tests). */
 typedef struct qdc_comm qdc_comm;
@@ -133,6 +134,12 @@ void qdc_comm_free(qdc_comm* comm);
 
 const char* qdc_circuit_new_sharded(qdc_circuit** out, size_t qubits_number, qdc_comm* comm);
 const char* qdc_circuit_new_local_shards(qdc_circuit** out, size_t qubits_number, int shards);
+/* One process driving one shard per listed device (ndev a power of two): distinct devices
+ * communicate through RCCL communicators made by ncclCommInitAll (collectives grouped over the
+ * shards' streams); the same device repeated keeps every shard on it, each on its own stream,
+ * exchanged by device copies ordered with events. */
+const char* qdc_circuit_new_devices(qdc_circuit** out, size_t qubits_number, int ndev,
+                                    const int* devices);
 
 /* Current layout of the forward state: phys[q] = physical bit of logical qubit q (n entries),
  * plus world size, this process's first rank and its number of local shards. */

@@ -74,14 +74,12 @@ def _free_port():
 
 
 def _rccl_worker(rank, world, port, q_out):
-    import torch.distributed as dist
     os.environ["LOCAL_RANK"] = str(rank)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
     try:
         import quantum_differentiable_circuit as q
         from quantum_differentiable_circuit.distributed import Communicator
-        comm = Communicator("f64")
+        comm = Communicator("f64", rank=rank, world=world,
+                            id_file=f"/tmp/qdc_test_rccl_{port}.id")
         n = 12
         ins, var = O.layered_circuit(n, 2, seed=7)
         c = build(q, "f64", n, ins, comm=comm)
@@ -91,8 +89,6 @@ def _rccl_worker(rank, world, port, q_out):
     except Exception:  # noqa: BLE001
         import traceback
         q_out.put((rank, None, None, traceback.format_exc()))
-    finally:
-        dist.destroy_process_group()
 
 
 def test_rccl_two_processes():
@@ -121,3 +117,45 @@ def test_rccl_two_processes():
     for _, d, g, _ in res:
         assert max(np.abs(a - b).max() for a, b in zip(d, dens)) < 1e-11
         assert normrel(np.concatenate(g), np.concatenate(grads)) < 1e-10
+
+
+def test_devices_multi_stream_one_gpu():
+    """qdc_circuit_new_devices with one device repeated: every shard on its own stream and
+    context (program copy, reduction arena), exchanged by copies ordered with events — the
+    single-process multi-GPU plumbing minus RCCL, on one GPU; equal to the oracle within 4x the
+    floor and to the single-stream loopback shards."""
+    import quantum_differentiable_circuit as q
+    n = 14
+    ins, var = O.layered_circuit(n, 4, seed=41)
+    fl = F.Floor("f32", n, ins, [], var, run=False)
+    for devs in ([0], [0, 0], [0, 0, 0, 0]):
+        c = build(q, "f32", n, ins, devices=devs)
+        d = c.forward([], fl.var)
+        fl.check("forward", d, f"C2 n={n} devices={devs} ")
+        fl.check("state", c.get_state(0), f"C2 n={n} devices={devs} ")
+        g = c.backward(fl.cots, [], fl.var)
+        fl.check("grads", g, f"C2 n={n} devices={devs} ")
+        fl.check("uncomputed", c.get_state(0), f"C2 n={n} devices={devs} ")
+        phys, world, _, nloc = c.layout()
+        assert world == len(devs) and nloc == len(devs)
+        if len(devs) > 1:
+            ref = build(q, "f32", n, ins, local_shards=len(devs))
+            dr = ref.forward([], fl.var)
+            F.check_pair("f32", d, dr, fl.floor["forward"], f"devices={devs} vs local shards")
+            F.check_pair("f32", g, ref.backward(fl.cots, [], fl.var), fl.floor["grads"],
+                         f"devices={devs} vs local shards grads")
+
+
+def test_devices_rccl_single_process():
+    """One process, one shard per GPU (ncclCommInitAll); skipped on a 1-GPU box (the driver's
+    multi-GPU bench runs bench.py --gpus N)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 GPUs")
+    import quantum_differentiable_circuit as q
+    n = 14
+    ins, var = O.layered_circuit(n, 3, seed=43)
+    fl = F.Floor("f64", n, ins, [], var, run=False)
+    c = build(q, "f64", n, ins, devices=2)
+    fl.check("forward", c.forward([], fl.var), "devices=2 ")
+    fl.check("grads", c.backward(fl.cots, [], fl.var), "devices=2 ")

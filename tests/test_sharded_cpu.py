@@ -254,3 +254,25 @@ def test_unpermute():
         pi = sum(((i >> q) & 1) << phys[q] for q in range(n))
         physical[pi] = psi[i]
     assert np.array_equal(unpermute(physical, phys), psi)
+
+
+def _id_worker(rank, path, q_out):
+    from quantum_differentiable_circuit.distributed import exchange_id
+    raw = exchange_id(rank, path, lambda: bytes(range(128)), timeout=60)
+    q_out.put((rank, raw))
+
+
+def test_rccl_id_file_exchange(tmp_path):
+    """The torch-free RCCL bootstrap (distributed.exchange_id): rank 0 publishes the 128-byte
+    id atomically, every other rank reads exactly it."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q_out = ctx.Queue()
+    path = tmp_path / "nccl.id"
+    ps = [ctx.Process(target=_id_worker, args=(r, path, q_out)) for r in (3, 2, 1, 0)]
+    for p in ps:
+        p.start()
+    got = dict(q_out.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == bytes(range(128)) for v in got.values()) and len(got) == 4
