@@ -224,6 +224,9 @@ struct Circuit {
   int rq_stats = 0;
   int rq_prefetch = 1;      // one-state register-resident passes prefetch the next tile (QDC_RQ_PF)
   int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
+  int rq_order = 0;  // register-resident tile order: 0 block-contiguous, 1 grid-strided (QDC_RQ_ORDER)
+  int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
+                    // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
@@ -279,6 +282,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_STATS")) rq_stats = atoi(e);
     if (const char* e = getenv("QDC_RQ_PF")) rq_prefetch = atoi(e);
     if (const char* e = getenv("QDC_RQ_PF2")) rq_prefetch2 = atoi(e);
+    if (const char* e = getenv("QDC_RW")) rq_wave = atoi(e);
+    if (const char* e = getenv("QDC_RQ_ORDER")) rq_order = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
@@ -892,6 +897,32 @@ struct Circuit {
                         const cx* mats, cx* partials, uint64_t stride) {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
+    if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
+      // one wave per tile (k_rw): lane l runs k_rq's threads l + 64 e
+      const bool pfw = two && (rq_wave & 4);
+      const void* kw = two ? (pfw ? (const void*)k_rw<true, 2, true> : (const void*)k_rw<true, 2, false>)
+                           : nt == 128 ? (const void*)k_rw<false, 2, false> : (const void*)k_rw<false, 4, false>;
+      uint32_t grid = 0;
+      QDC_TRY(fused_grid(fg, kw, 64, grid));
+      fgeo g = fg;
+      uint64_t tpb = 1;
+      while (tpb * grid < g.ntiles) tpb <<= 1;
+      g.tpb = (uint32_t)tpb;
+      grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+      if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
+      last_fused_grid = grid;
+      if (two && pfw)
+        return ctx.launch_block(name, bytes, k_rw<true, 2, true>, grid, 64u, f, b, fops, mats, g,
+                                l0, partials, stride);
+      if (two)
+        return ctx.launch_block(name, bytes, k_rw<true, 2, false>, grid, 64u, f, b, fops, mats, g,
+                                l0, partials, stride);
+      if (nt == 128)
+        return ctx.launch_block(name, bytes, k_rw<false, 2, false>, grid, 64u, f, b, fops, mats, g,
+                                l0, partials, stride);
+      return ctx.launch_block(name, bytes, k_rw<false, 4, false>, grid, 64u, f, b, fops, mats, g,
+                              l0, partials, stride);
+    }
     const void* kern = nullptr;
     // the next tile's loads are in flight while this tile's stages run (2 waves/SIMD)
     const bool pf = two ? rq_prefetch2 != 0 : rq_prefetch != 0;
@@ -952,6 +983,7 @@ struct Circuit {
   // stages, densities) go to slots it.grad_slots of red_base (grads or dens of each shard).
   const char* run_fused(const Item& it, bool two, size_t mats_off, bool red_to_grads) {
     fgeo fg{};
+    fg.order = it.rq ? (uint32_t)rq_order : 0u;
     fg.lc = it.lc;
     fg.h = it.h;
     for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];

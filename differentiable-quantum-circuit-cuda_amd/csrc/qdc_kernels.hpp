@@ -578,6 +578,7 @@ struct fgeo {
   uint32_t hb[FMAX_ROWS];
   uint32_t nops;
   uint32_t ngrad;  // reduction ops (Gamma stages, densities): partials in consecutive slots
+  uint32_t order;  // register-resident passes: 0 block-contiguous tiles, 1 grid-strided
 };
 
 // Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the

@@ -66,18 +66,18 @@ __device__ __forceinline__ constexpr int rq_base(int k) {  // k-th index with bi
     if ((k >> bit) & 1) b |= 1 << s;
     ++bit;
   }
-  return b;
+  return b | ((k >> 2) << 4);  // registers beyond 16 (k_rw): bits above the four slots
 }
 
 // two-qubit stage on registers: f <- A f [, Gamma += b0 f0^T, b <- B b]
-template <int S1, int S2, bool TWO>
-__device__ __forceinline__ void rq_q2(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+template <int S1, int S2, bool TWO, int R>
+__device__ __forceinline__ void rq_q2(cx (&f)[R], cx (&b)[R], const cx* __restrict__ M,
                                       bool gamma, real* acc_out) {
   cx A[16], B[16];
   if (TWO && gamma) {
     cx acc[16];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < R / 4; ++k) {
       const int base = rq_base<S1, S2>(k);
 #pragma unroll
       for (int p = 0; p < 4; ++p)
@@ -99,7 +99,7 @@ __device__ __forceinline__ void rq_q2(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
   for (int i = 0; i < 16; ++i) A[i] = M[i];
   // f with A, then b with B: one matrix (32 SGPRs) live at a time
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < R / 4; ++k) {
     const int base = rq_base<S1, S2>(k);
     cx x[4];
 #pragma unroll
@@ -112,7 +112,7 @@ __device__ __forceinline__ void rq_q2(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
 #pragma unroll
     for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < R / 4; ++k) {
       const int base = rq_base<S1, S2>(k);
       cx x[4];
 #pragma unroll
@@ -125,8 +125,8 @@ __device__ __forceinline__ void rq_q2(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
 }
 
 // diagonal two-qubit stage: element r = 2 bit(t2) + bit(t1) of each quartet takes entry r
-template <int S1, int S2, bool TWO>
-__device__ __forceinline__ void rq_diag(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+template <int S1, int S2, bool TWO, int R>
+__device__ __forceinline__ void rq_diag(cx (&f)[R], cx (&b)[R], const cx* __restrict__ M,
                                         bool gamma, real* acc_out) {
   cx A[4], B[4];
 #pragma unroll
@@ -138,7 +138,7 @@ __device__ __forceinline__ void rq_diag(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* 
   if (TWO && gamma) {
     cx acc[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < R / 4; ++k) {
       const int base = rq_base<S1, S2>(k);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -155,7 +155,7 @@ __device__ __forceinline__ void rq_diag(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* 
     wave_reduce_add<8>(v, acc_out);
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < R / 4; ++k) {
     const int base = rq_base<S1, S2>(k);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -167,8 +167,8 @@ __device__ __forceinline__ void rq_diag(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* 
 }
 
 // one-qubit stage on slot S: pairs (j, j | 1 << S)
-template <int S, bool TWO>
-__device__ __forceinline__ void rq_q1(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __restrict__ M,
+template <int S, bool TWO, int R>
+__device__ __forceinline__ void rq_q1(cx (&f)[R], cx (&b)[R], const cx* __restrict__ M,
                                       bool gamma, real* acc_out) {
   cx A[4], B[4];
 #pragma unroll
@@ -181,7 +181,7 @@ __device__ __forceinline__ void rq_q1(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
   if (TWO && gamma) {
     cx acc[4];
 #pragma unroll
-    for (int k = 0; k < RQ_R / 2; ++k) {
+    for (int k = 0; k < R / 2; ++k) {
       const int j0 = ((k & ~LOWM) << 1) | (k & LOWM), j1 = j0 | (1 << S);
       const cx bx[2] = {b[j0], b[j1]}, fx[2] = {f[j0], f[j1]};
 #pragma unroll
@@ -199,7 +199,7 @@ __device__ __forceinline__ void rq_q1(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
     wave_reduce_add<8>(v, acc_out);
   }
 #pragma unroll
-  for (int k = 0; k < RQ_R / 2; ++k) {
+  for (int k = 0; k < R / 2; ++k) {
     const int j0 = ((k & ~LOWM) << 1) | (k & LOWM), j1 = j0 | (1 << S);
     cx x[2] = {f[j0], f[j1]};
     umatvec<2>(A, x);
@@ -211,6 +211,43 @@ __device__ __forceinline__ void rq_q1(cx (&f)[RQ_R], cx (&b)[RQ_R], const cx* __
       b[j0] = y[0];
       b[j1] = y[1];
     }
+  }
+}
+
+// one register stage: slot case (host: rq_plan) two-qubit / diagonal S1 * 4 + S2 (t1 in slot
+// S1, t2 in slot S2); one-qubit: the slot of t1
+template <bool TWO, int R>
+__device__ __forceinline__ void rq_stage(uint32_t sel, cx (&xf)[R], cx (&xb)[R],
+                                         const cx* __restrict__ M, bool gamma, real* acc) {
+  switch (sel) {
+    case FK_Q2 * 16 + 1: rq_q2<0, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 2: rq_q2<0, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 3: rq_q2<0, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 4: rq_q2<1, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 6: rq_q2<1, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 7: rq_q2<1, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 8: rq_q2<2, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 9: rq_q2<2, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 11: rq_q2<2, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 12: rq_q2<3, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 13: rq_q2<3, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q2 * 16 + 14: rq_q2<3, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 1: rq_diag<0, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 2: rq_diag<0, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 3: rq_diag<0, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 4: rq_diag<1, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 6: rq_diag<1, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 7: rq_diag<1, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 8: rq_diag<2, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 9: rq_diag<2, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 11: rq_diag<2, 3, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 12: rq_diag<3, 0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 13: rq_diag<3, 1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_DIAG * 16 + 14: rq_diag<3, 2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 16 + 0: rq_q1<0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 16 + 1: rq_q1<1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 16 + 2: rq_q1<2, TWO, R>(xf, xb, M, gamma, acc); break;
+    default: rq_q1<3, TWO, R>(xf, xb, M, gamma, acc); break;
   }
 }
 
@@ -310,6 +347,64 @@ __device__ __forceinline__ void rq_vmwait_two(uint32_t first, vec16 (&v)[8], vec
                : "memory", "scc");
 }
 
+
+// k_rw prefetch: the next tile's 32 chunks in AGPRs a[0:127] (one wave per SIMD: 256 VGPRs +
+// 256 AGPRs), loaded and waited for as in rq_ld / rq_vmwait_two (hidden from the waitcnt pass,
+// pinned registers, a tied wait).  The wait covers all 32 chunks; the second statement only
+// re-defines a[64:127] after it (asm volatile statements keep their order).
+template <int REG>
+__device__ __forceinline__ vec16 rw_lda(const chunk* p) {
+  vec16 v;
+  switch (REG) {
+    case 0: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[0:3]}"(v) : "v"(p) : "memory"); break;
+    case 4: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[4:7]}"(v) : "v"(p) : "memory"); break;
+    case 8: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[8:11]}"(v) : "v"(p) : "memory"); break;
+    case 12: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[12:15]}"(v) : "v"(p) : "memory"); break;
+    case 16: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[16:19]}"(v) : "v"(p) : "memory"); break;
+    case 20: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[20:23]}"(v) : "v"(p) : "memory"); break;
+    case 24: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[24:27]}"(v) : "v"(p) : "memory"); break;
+    case 28: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[28:31]}"(v) : "v"(p) : "memory"); break;
+    case 32: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[32:35]}"(v) : "v"(p) : "memory"); break;
+    case 36: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[36:39]}"(v) : "v"(p) : "memory"); break;
+    case 40: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[40:43]}"(v) : "v"(p) : "memory"); break;
+    case 44: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[44:47]}"(v) : "v"(p) : "memory"); break;
+    case 48: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[48:51]}"(v) : "v"(p) : "memory"); break;
+    case 52: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[52:55]}"(v) : "v"(p) : "memory"); break;
+    case 56: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[56:59]}"(v) : "v"(p) : "memory"); break;
+    case 60: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[60:63]}"(v) : "v"(p) : "memory"); break;
+    case 64: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[64:67]}"(v) : "v"(p) : "memory"); break;
+    case 68: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[68:71]}"(v) : "v"(p) : "memory"); break;
+    case 72: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[72:75]}"(v) : "v"(p) : "memory"); break;
+    case 76: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[76:79]}"(v) : "v"(p) : "memory"); break;
+    case 80: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[80:83]}"(v) : "v"(p) : "memory"); break;
+    case 84: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[84:87]}"(v) : "v"(p) : "memory"); break;
+    case 88: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[88:91]}"(v) : "v"(p) : "memory"); break;
+    case 92: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[92:95]}"(v) : "v"(p) : "memory"); break;
+    case 96: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[96:99]}"(v) : "v"(p) : "memory"); break;
+    case 100: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[100:103]}"(v) : "v"(p) : "memory"); break;
+    case 104: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[104:107]}"(v) : "v"(p) : "memory"); break;
+    case 108: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[108:111]}"(v) : "v"(p) : "memory"); break;
+    case 112: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[112:115]}"(v) : "v"(p) : "memory"); break;
+    case 116: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[116:119]}"(v) : "v"(p) : "memory"); break;
+    case 120: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[120:123]}"(v) : "v"(p) : "memory"); break;
+    case 124: asm volatile("global_load_dwordx4 %0, %1, off nt" : "={a[124:127]}"(v) : "v"(p) : "memory"); break;
+  }
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void rw_vmwait(uint32_t first, vec16 (&v)[32]) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  const uint32_t fs = __builtin_amdgcn_readfirstlane(first);
+  asm volatile(QDC_RQ_WAIT_ASM
+               : "+{a[0:3]}"(v[0]), "+{a[4:7]}"(v[1]), "+{a[8:11]}"(v[2]), "+{a[12:15]}"(v[3]), "+{a[16:19]}"(v[4]), "+{a[20:23]}"(v[5]), "+{a[24:27]}"(v[6]), "+{a[28:31]}"(v[7]), "+{a[32:35]}"(v[8]), "+{a[36:39]}"(v[9]), "+{a[40:43]}"(v[10]), "+{a[44:47]}"(v[11]), "+{a[48:51]}"(v[12]), "+{a[52:55]}"(v[13]), "+{a[56:59]}"(v[14]), "+{a[60:63]}"(v[15])
+               : [first] "s"(fs), [cnt] "n"(N)
+               : "memory", "scc");
+  asm volatile(""
+               : "+{a[64:67]}"(v[16]), "+{a[68:71]}"(v[17]), "+{a[72:75]}"(v[18]), "+{a[76:79]}"(v[19]), "+{a[80:83]}"(v[20]), "+{a[84:87]}"(v[21]), "+{a[88:91]}"(v[22]), "+{a[92:95]}"(v[23]), "+{a[96:99]}"(v[24]), "+{a[100:103]}"(v[25]), "+{a[104:107]}"(v[26]), "+{a[108:111]}"(v[27]), "+{a[112:115]}"(v[28]), "+{a[116:119]}"(v[29]), "+{a[120:123]}"(v[30]), "+{a[124:127]}"(v[31])
+               :
+               : "memory");
+}
+
 // TWO: fwd and bwd (reverse sweep, Gamma stages reduce into partials); else fwd only.
 // fg.nops ops at `ops`; at mats + l0 the load layout's descriptor, then rqio.
 #ifndef QDC_RQ_PF_WAVES
@@ -345,9 +440,15 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       thr_st += io->gv_st[k];
     }
   }
-  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
+  // block-contiguous tiles (tile0 + s) or grid-strided (tile0 + s * grid: concurrently running
+  // tiles are neighbours in memory)
+  const bool gstride = fg.order != 0;
+  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * fg.tpb;
+  const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
   const uint32_t count =
-      tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+      tile0 >= fg.ntiles ? 0u
+      : gstride          ? (uint32_t)((fg.ntiles - 1 - tile0) / tstep + 1)
+                         : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
   auto tile_base = [&](uint64_t tile) {
     uint64_t base = tile << fg.lc;
 #pragma unroll
@@ -429,45 +530,14 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         lcur = op.mat;
         continue;
       }
-      // slot case (host: rq_plan): two-qubit / diagonal S1 * 4 + S2 (t1 in slot S1, t2 in
-      // slot S2); one-qubit: the slot of t1
-      switch (kind * 16u + op.t1) {
-        case FK_Q2 * 16 + 1: rq_q2<0, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 2: rq_q2<0, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 3: rq_q2<0, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 4: rq_q2<1, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 6: rq_q2<1, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 7: rq_q2<1, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 8: rq_q2<2, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 9: rq_q2<2, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 11: rq_q2<2, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 12: rq_q2<3, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 13: rq_q2<3, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q2 * 16 + 14: rq_q2<3, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 1: rq_diag<0, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 2: rq_diag<0, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 3: rq_diag<0, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 4: rq_diag<1, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 6: rq_diag<1, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 7: rq_diag<1, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 8: rq_diag<2, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 9: rq_diag<2, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 11: rq_diag<2, 3, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 12: rq_diag<3, 0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 13: rq_diag<3, 1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_DIAG * 16 + 14: rq_diag<3, 2, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q1 * 16 + 0: rq_q1<0, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q1 * 16 + 1: rq_q1<1, TWO>(xf, xb, M, gamma, acc); break;
-        case FK_Q1 * 16 + 2: rq_q1<2, TWO>(xf, xb, M, gamma, acc); break;
-        default: rq_q1<3, TWO>(xf, xb, M, gamma, acc); break;
-      }
+      rq_stage<TWO>(kind * 16u + op.t1, xf, xb, M, gamma, acc);
       if (gamma) ++ri;
     }
   };
   if constexpr (!PF) {
     cx xf[RQ_R], xb[RQ_R];
     for (uint32_t tt = 0; tt < count; ++tt) {
-      const uint64_t base = tile_base(tile0 + tt);
+      const uint64_t base = tile_base(tile0 + tt * tstep);
       load(xf, xb, base);
       run(xf, xb);
       store(xf, xb, base);
@@ -519,7 +589,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       take();
       const uint64_t prev = cur;
       if (s < count) {
-        cur = tile_base(tile0 + s);
+        cur = tile_base(tile0 + s * tstep);
         issue(cur);
       }
       if (s > 0) {
@@ -536,6 +606,233 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #pragma unroll
       for (int w = 0; w < NT / 64; ++w) s += accw[w][k][e];
       reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] = s;
+    }
+  }
+}
+
+// One wave per tile (k_rw): the same programs, layouts and HBM addressing as k_rq with NT
+// threads, run by one 64-lane wave.  Lane l holds the registers of k_rq's threads l + 64 e
+// (e < NE = NT / 64) as its registers j + 16 e: k_rq's thread bits 6.. become register bits
+// 4.. that no stage addresses (the host plan is unchanged).  What changes:
+//  * a relayout is wave-local — LDS accesses of one wave execute in order, so it needs no
+//    barrier (k_rq: two per relayout and state, coupling the tile's waves);
+//  * every Gamma stage accumulates NE times the amplitudes per lane before its one 64-lane
+//    reduce-scatter (the reduction's cost per amplitude divides by NE);
+//  * waves are independent: while one computes, another on the SIMD loads or stores.
+// Registers: R = 16 NE amplitudes per state and lane (two-state NE = 2: 128 VGPRs of tile;
+// one-state NE = 4: 128), so 2 waves/SIMD.
+#ifndef QDC_RW_WAVES
+#define QDC_RW_WAVES 2
+#endif
+template <bool TWO, int NE, bool PF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 1 : QDC_RW_WAVES, PF ? 1 : QDC_RW_WAVES)))
+void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
+          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
+          uint64_t slot_stride) {
+  static_assert(NE == 2 || NE == 4, "k_rw: 2 or 4 register groups");
+  constexpr int LOGNE = NE == 2 ? 1 : 2;
+  constexpr int R = RQ_R * NE;   // amplitudes per lane and state
+  constexpr int CPT = R / VEC;   // chunks per lane and state
+  constexpr int CPG = RQ_R / VEC;  // chunks per register group (8)
+  __shared__ cx buf[64 * R];
+  __shared__ real accw[TWO ? FMAX_GRAD_RQ : 1][FACC];
+  const uint32_t lane = threadIdx.x;
+  if constexpr (TWO) {
+    for (uint32_t i = lane; i < FMAX_GRAD_RQ * FACC; i += 64) (&accw[0][0])[i] = 0;
+  }
+  const rqio* io = reinterpret_cast<const rqio*>(mats + l0 + sizeof(rq_layout) / sizeof(cx));
+  uint64_t thr_ld = 0, thr_st = 0;  // this lane's chunk offsets in the load / store layout
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if ((lane >> k) & 1u) {
+      thr_ld += io->gv_ld[k];
+      thr_st += io->gv_st[k];
+    }
+  }
+  // block-contiguous tiles (tile0 + s) or grid-strided (tile0 + s * grid: concurrently running
+  // tiles are neighbours in memory)
+  const bool gstride = fg.order != 0;
+  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * fg.tpb;
+  const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
+  const uint32_t count =
+      tile0 >= fg.ntiles ? 0u
+      : gstride          ? (uint32_t)((fg.ntiles - 1 - tile0) / tstep + 1)
+                         : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+  auto tile_base = [&](uint64_t tile) {
+    uint64_t base = tile << fg.lc;
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
+    return base;
+  };
+  auto rqio_now = [&]() {
+    uint32_t ro = l0;
+    asm volatile("" : "+s"(ro));
+    return reinterpret_cast<const rqio*>(mats + ro + sizeof(rq_layout) / sizeof(cx));
+  };
+  // register group e (k_rq's thread bits 6.. = e): chunk offset sum of gv[6 + i] over e's bits
+  auto goff = [&](const uint64_t* gv, int e) {
+    uint64_t o = 0;
+#pragma unroll
+    for (int i = 0; i < LOGNE; ++i)
+      if ((e >> i) & 1) o += gv[6 + i];
+    return o;
+  };
+  auto load = [&](cx (&xf)[R], cx (&xb)[R], uint64_t base) __attribute__((always_inline)) {
+    const rqio* rg = rqio_now();
+    const chunk* pf = f + (base + thr_ld);
+    const chunk* pb = b + (base + thr_ld);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const uint64_t eo = goff(rg->gv_ld, e);
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const chunk cf = ldc(pf + (eo + rg->offi_ld[i]));
+        xf[16 * e + 2 * i] = cf.v[0];
+        xf[16 * e + 2 * i + 1] = cf.v[1];
+        if constexpr (TWO) {
+          const chunk cb = ldc(pb + (eo + rg->offi_ld[i]));
+          xb[16 * e + 2 * i] = cb.v[0];
+          xb[16 * e + 2 * i + 1] = cb.v[1];
+        }
+      }
+    }
+  };
+  auto store = [&](cx (&xf)[R], cx (&xb)[R], uint64_t base) __attribute__((always_inline)) {
+    const rqio* rg = rqio_now();
+    chunk* pf = f + (base + thr_st);
+    chunk* pb = b + (base + thr_st);
+    asm volatile("" : "+v"(pf), "+v"(pb));
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const uint64_t eo = goff(rg->gv_st, e);
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        chunk c;
+        c.v[0] = xf[16 * e + 2 * i];
+        c.v[1] = xf[16 * e + 2 * i + 1];
+        stc(pf + (eo + rg->offi_st[i]), c);
+        if constexpr (TWO) {
+          c.v[0] = xb[16 * e + 2 * i];
+          c.v[1] = xb[16 * e + 2 * i + 1];
+          stc(pb + (eo + rg->offi_st[i]), c);
+        }
+      }
+    }
+  };
+  // one state from layout Lc to Ln through the wave's LDS buffer: LDS operations of a wave
+  // complete in issue order, so the reads see every lane's writes without a barrier, and the
+  // next relayout's writes come after these reads
+  auto exchange = [&](cx (&x)[R], uint32_t tp, const rq_layout* Lc, uint32_t tpn,
+                      const rq_layout* Ln) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      uint32_t te = 0;
+#pragma unroll
+      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Lc->tv[6 + i] : 0u;
+#pragma unroll
+      for (int j = 0; j < RQ_R; ++j) buf[(tp ^ te) ^ Lc->rp[j]] = x[16 * e + j];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      uint32_t te = 0;
+#pragma unroll
+      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Ln->tv[6 + i] : 0u;
+#pragma unroll
+      for (int j = 0; j < RQ_R; ++j) x[16 * e + j] = buf[(tpn ^ te) ^ Ln->rp[j]];
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto run = [&](cx (&xf)[R], cx (&xb)[R]) __attribute__((always_inline)) {
+    uint32_t lcur = l0;
+    uint32_t ri = 0;
+    for (uint32_t j = 0; j < fg.nops; ++j) {
+      const fop op = ops[j];
+      const uint32_t kind = op.kind & 7u;
+      const bool gamma = TWO && (op.kind & FOP_GAMMA) && !(QDC_RQ_ABL & 4);
+      const cx* M = mats + op.mat;
+      real* acc = TWO ? &accw[ri][0] : nullptr;
+      if ((QDC_RQ_ABL & 2) && kind == FK_RELAYOUT) {
+        lcur = op.mat;
+        continue;
+      }
+      if ((QDC_RQ_ABL & 1) && kind != FK_RELAYOUT) {
+        if (TWO && (op.kind & FOP_GAMMA)) ++ri;
+        continue;
+      }
+      if (kind == FK_RELAYOUT) {
+        const rq_layout* Lc = reinterpret_cast<const rq_layout*>(mats + lcur);
+        const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
+        const uint32_t tp = rq_tp<6>(Lc, lane), tpn = rq_tp<6>(Ln, lane);
+        exchange(xf, tp, Lc, tpn, Ln);
+        if constexpr (TWO) exchange(xb, tp, Lc, tpn, Ln);
+        lcur = op.mat;
+        continue;
+      }
+      rq_stage<TWO>(kind * 16u + op.t1, xf, xb, M, gamma, acc);
+      if (gamma) ++ri;
+    }
+  };
+  cx xf[R], xb[R];  // xb unused (eliminated) in one-state passes
+  if constexpr (!PF) {
+    for (uint32_t tt = 0; tt < count; ++tt) {
+      const uint64_t base = tile_base(tile0 + tt * tstep);
+      load(xf, xb, base);
+      run(xf, xb);
+      store(xf, xb, base);
+    }
+  } else {
+    static_assert(TWO && NE == 2, "k_rw prefetch: two-state tiles (32 chunks in a[0:127])");
+    constexpr int NLD = 2 * CPT;  // vector-memory ops per tile: loads = stores
+    vec16 pf[2 * CPT];            // chunk i of fwd at pf[i], of bwd at pf[CPT + i]
+    auto issue = [&](uint64_t base) __attribute__((always_inline)) {
+      const rqio* rg = rqio_now();
+      const chunk* pfp = f + (base + thr_ld);
+      const chunk* pbp = b + (base + thr_ld);
+      const uint64_t e1 = rg->gv_ld[6];
+#define QDC_RW_ISSUE(i)                                                                   \
+  pf[i] = rw_lda<4 * (i)>(pfp + (((i) >= 8 ? e1 : 0) + rg->offi_ld[(i) & 7]));            \
+  pf[CPT + (i)] = rw_lda<4 * (CPT + (i))>(pbp + (((i) >= 8 ? e1 : 0) + rg->offi_ld[(i) & 7]));
+      QDC_RW_ISSUE(0) QDC_RW_ISSUE(1) QDC_RW_ISSUE(2) QDC_RW_ISSUE(3)
+      QDC_RW_ISSUE(4) QDC_RW_ISSUE(5) QDC_RW_ISSUE(6) QDC_RW_ISSUE(7)
+      QDC_RW_ISSUE(8) QDC_RW_ISSUE(9) QDC_RW_ISSUE(10) QDC_RW_ISSUE(11)
+      QDC_RW_ISSUE(12) QDC_RW_ISSUE(13) QDC_RW_ISSUE(14) QDC_RW_ISSUE(15)
+#undef QDC_RW_ISSUE
+    };
+    auto take = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {  // chunk i = register group i / 8, pair i % 8
+        const chunk c = __builtin_bit_cast(chunk, pf[i]);
+        const chunk d = __builtin_bit_cast(chunk, pf[CPT + i]);
+        xf[2 * i] = c.v[0];
+        xf[2 * i + 1] = c.v[1];
+        xb[2 * i] = d.v[0];
+        xb[2 * i + 1] = d.v[1];
+      }
+    };
+    // as k_rq's PF loop: step s takes tile s-1, issues tile s, runs and stores tile s-1
+    uint64_t cur = 0;
+    for (uint32_t s = 0; s <= count; ++s) {
+      rw_vmwait<NLD>(s <= 1 ? 1u : 0u, pf);
+      take();
+      const uint64_t prev = cur;
+      if (s < count) {
+        cur = tile_base(tile0 + s * tstep);
+        issue(cur);
+      }
+      if (s > 0) {
+        run(xf, xb);
+        store(xf, xb, prev);
+      }
+    }
+  }
+  if constexpr (TWO) {
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < fg.ngrad * FACC; i += 64) {
+      const uint32_t k = i / FACC, e = i % FACC;
+      reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] =
+          accw[k][e];
     }
   }
 }

@@ -164,11 +164,24 @@ def build_env(prec, n, ins, env):
     return c
 
 
+# register-resident variants (csrc/qdc_rq.hpp): k_rq (a tile per block of NT threads, QDC_RW=0),
+# k_rw (a tile per wave; bit 0 two-state, bit 1 one-state, bit 2 two-state with the next tile
+# prefetched into AGPRs), and the grid-strided tile order
+RQ_VARIANTS = {
+    "lds": {"QDC_RQ": 0},
+    "k_rq": {"QDC_RQ": 1, "QDC_RW": 0},
+    "k_rw": {"QDC_RQ": 1, "QDC_RW": 1},
+    "k_rw_all": {"QDC_RQ": 1, "QDC_RW": 3},
+    "k_rw_pf": {"QDC_RQ": 1, "QDC_RW": 5},
+    "k_rw_gstride": {"QDC_RQ": 1, "QDC_RW": 1, "QDC_RQ_ORDER": 1},
+}
+
+
 @pytest.mark.parametrize("case", ["layered12", "layered16", "random12", "random17"])
 def test_register_resident_passes_equal_lds_passes(case):
-    """f32 gate passes run register-resident (k_rq, csrc/qdc_rq.hpp: relayouts through LDS,
-    stages on VGPRs) by default; QDC_RQ=0 keeps them in LDS tiles (k_fused).  Both must agree
-    with each other and with the oracle, forward and reverse sweep."""
+    """f32 gate passes run register-resident (csrc/qdc_rq.hpp: relayouts through LDS, stages
+    on VGPRs) by default; QDC_RQ=0 keeps them in LDS tiles (k_fused).  Every variant of
+    RQ_VARIANTS must agree with the oracle and with the LDS passes, forward and reverse sweep."""
     kind, n = case[:-2], int(case[-2:])
     if kind == "layered":
         ins, var = O.layered_circuit(n, 4, seed=24)
@@ -179,18 +192,22 @@ def test_register_resident_passes_equal_lds_passes(case):
         psi0 = O.random_state(np.random.default_rng(n), n)
     fl = F.Floor("f32", n, ins, const, var, psi0=psi0, run=False)
     res = {}
-    for rq in (0, 1):
-        c = build_env("f32", n, ins, {"QDC_RQ": rq, "QDC_FUSE": 1})
+    for name, env in RQ_VARIANTS.items():
+        c = build_env("f32", n, ins, dict(env, QDC_FUSE=1))
         if psi0 is not None:
             c.set_state_from_vector(fl.psi0)
         d = c.forward(fl.const, fl.var)
         g = c.backward(fl.cots, fl.const, fl.var)
-        what = f"{case} QDC_RQ={rq} "
+        what = f"{case} {name} "
         fl.check("forward", d, what)
         fl.check("grads", g, what)
         fl.check("uncomputed", c.get_state(0), what)
-        res[rq] = (d, g)
-    F.check_pair("f32", res[1][1], res[0][1], fl.floor["grads"], f"{case} rq vs lds grads")
+        res[name] = (d, g)
+    for name in RQ_VARIANTS:
+        if name != "lds":
+            F.check_pair("f32", res[name][1], res["lds"][1], fl.floor["grads"],
+                         f"{case} {name} vs lds grads")
+
 
 @pytest.mark.parametrize("n,perm_low", [(13, 0), (18, 0), (18, 6), (18, 8)])
 def test_permuting_passes_equal_fixed_layout(n, perm_low):

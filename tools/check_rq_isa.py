@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Check the prefetching register-resident kernels (qdc_rq.hpp, k_rq<*, *, true>): no
+"""Check the prefetching register-resident kernels (qdc_rq.hpp, k_rq<*, *, true> and
+k_rw<*, *, true>, VGPR and AGPR destinations): no
 instruction may read or overwrite the destination registers of a hidden prefetch load
 (inline-asm global_load_dwordx4 ... nt) on any control-flow path between the load and the
 explicit asm s_waitcnt vmcnt that retires it (a copy or spill of an in-flight register would
@@ -17,11 +18,12 @@ text = open(path).read().splitlines()
 
 
 def regs(tok):
-    m = re.match(r"-?v\[(\d+):(\d+)\]", tok)
+    """VGPRs and AGPRs named by an operand, as (class, index)."""
+    m = re.match(r"-?([va])\[(\d+):(\d+)\]", tok)
     if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
-    m = re.match(r"-?v(\d+)$", tok)
-    return {int(m.group(1))} if m else set()
+        return {(m.group(1), k) for k in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r"-?([va])(\d+)$", tok)
+    return {(m.group(1), int(m.group(2)))} if m else set()
 
 
 def parse(line):
@@ -49,7 +51,7 @@ def reads_writes(op, ops):
 
 bad = 0
 for start, line in enumerate(text):
-    m = re.match(r"^(_ZN3qdc4k_rqILb[01]ELi\d+ELb1E\S*):", line)
+    m = re.match(r"^(_ZN3qdc4k_r[qw]ILb[01]ELi\d+ELb1E\S*):", line)
     if not m:
         continue
     name = m.group(1)
