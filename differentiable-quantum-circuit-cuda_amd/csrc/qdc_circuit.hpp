@@ -850,6 +850,25 @@ struct Circuit {
           F = pf[step.stage];
           F.t1 = step.cs;
           F.t2 = 0;
+          // two-qubit / diagonal stages run with the lower slot first (half the kernel's
+          // cases): exchange t1 and t2 by permuting the matrices' index bits, and the
+          // stage's Gamma back on the host
+          const uint32_t kd = F.kind & 7u;
+          if ((kd == FK_Q2 || kd == FK_DIAG) && (step.cs >> 2) > (step.cs & 3u)) {
+            F.t1 = (step.cs & 3u) * 4u + (step.cs >> 2);
+            const int nm = kd == FK_DIAG ? 4 : 16;
+            for (int h = 0; h < 2; ++h) {  // A, then B
+              cx* m = &mats[F.mat + (size_t)h * nm];
+              cx t[16];
+              for (int i = 0; i < nm; ++i) t[i] = m[i];
+              for (int i = 0; i < nm; ++i)
+                m[i] = kd == FK_DIAG ? t[swap_bits4(i)]
+                                     : t[swap_bits4(i >> 2) * 4 + swap_bits4(i & 3)];
+            }
+            if (pslot[step.stage] >= 0)
+              for (StagePost& sp : stage_post)
+                if (sp.slot == (uint32_t)pslot[step.stage]) sp.swapped = true;
+          }
         }
         fops[fo++] = F;
         ++n;
@@ -1279,9 +1298,16 @@ struct Circuit {
       for (const StagePost& st : stage_post) {
         SMat G = smat_identity(st.R);
         const cx* g = host_out + (size_t)st.slot * RED;
+        auto sw = [&](int p) { return st.swapped ? swap_bits4(p) : p; };
         if (st.diag_only) {
           for (int i = 0; i < 16; ++i) G.a[i] = 0;
-          for (int r = 0; r < 4; ++r) G.a[r * 4 + r] = cd(g[r].x, g[r].y);
+          for (int r = 0; r < 4; ++r) G.a[r * 4 + r] = cd(g[sw(r)].x, g[sw(r)].y);
+        } else if (st.R == 4) {
+          for (int p = 0; p < 4; ++p)
+            for (int q = 0; q < 4; ++q) {
+              const cx v = g[sw(p) * 4 + sw(q)];
+              G.a[p * 4 + q] = cd(v.x, v.y);
+            }
         } else {
           for (int i = 0; i < st.R * st.R; ++i) G.a[i] = cd(g[i].x, g[i].y);
         }

@@ -65,12 +65,16 @@ struct diag4 {
 };
 
 // nontemporal 16-byte chunk access (streams larger than every cache level)
+// Every state lives in global memory: the accesses go through address space 1, so they stay
+// global_load/store even where a laundered pointer (asm "+v") lost the address space
+// (flat_* would also count in lgkmcnt and complete out of order).
+typedef __attribute__((address_space(1))) vec16 gvec16;
 __device__ __forceinline__ chunk ldc(const chunk* p) {
-  const vec16 v = __builtin_nontemporal_load(reinterpret_cast<const vec16*>(p));
+  const vec16 v = __builtin_nontemporal_load((const gvec16*)(p));
   return __builtin_bit_cast(chunk, v);
 }
 __device__ __forceinline__ void stc(chunk* p, const chunk& c) {
-  __builtin_nontemporal_store(__builtin_bit_cast(vec16, c), reinterpret_cast<vec16*>(p));
+  __builtin_nontemporal_store(__builtin_bit_cast(vec16, c), (gvec16*)(p));
 }
 
 __device__ __forceinline__ cx cmul(cx a, cx b) {
@@ -718,7 +722,7 @@ __device__ __forceinline__ void half_swap(double& a, double& b) {
 // ATOMIC: several waves add into the same LDS accumulators (ds_add_f32)
 // Timing-only ablation builds (tools/ablate.sh; results are wrong): QDC_RQ_ABL bit 0 no stage
 // math, bit 1 no relayouts, bit 2 no Gamma, bit 3 Gamma without the wave reduction, bit 4
-// relayouts without barriers (qdc_rq.hpp).
+// relayouts without barriers, bit 5 no HBM loads/stores (k_rw; qdc_rq.hpp).
 #ifndef QDC_RQ_ABL
 #define QDC_RQ_ABL 0
 #endif
@@ -751,12 +755,22 @@ __device__ __forceinline__ void wave_reduce_add(real (&x)[V], real* acc) {
       const int half = len >> 1;
 #pragma unroll
       for (int i = 0; i < half; ++i) {
-        if (step == 0) {
-          half_swap<32>(x[i], x[half + i]);
+        if (step <= 1) {
+          if (step == 0) half_swap<32>(x[i], x[half + i]);
+          else half_swap<16>(x[i], x[half + i]);
+#ifndef QDC_F64
+          if (i & 1) {  // f32: the adds of value pairs (i - 1, i) as one v_pk_add_f32
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            f2 a = {x[i - 1], x[i]}, c = {x[half + i - 1], x[half + i]};
+            a += c;
+            x[i - 1] = a.x;
+            x[i] = a.y;
+          } else if (i == half - 1) {
+            x[i] += x[half + i];
+          }
+#else
           x[i] += x[half + i];
-        } else if (step == 1) {
-          half_swap<16>(x[i], x[half + i]);
-          x[i] += x[half + i];
+#endif
         } else {
           const real mine = lane_sel(x[i], x[half + i], UPPER[step]);
           const real send = lane_sel(x[half + i], x[i], UPPER[step]);

@@ -148,6 +148,9 @@ struct StagePost {
   uint32_t slot;
   int R;           // 2 or 4
   bool diag_only;  // Gamma holds only its diagonal (4 values)
+  // register-resident pass run with t1/t2 exchanged (slot case S1 < S2, qdc_rq.hpp): the
+  // kernel's Gamma index bits are swapped (Gamma[p][q] = got[swap p][swap q])
+  bool swapped = false;
   std::vector<StageGate> gates;
 };
 
