@@ -917,12 +917,13 @@ struct Circuit {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
-      // one wave per tile (k_rw): lane l runs k_rq's threads l + 64 e
+      // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);
-      const void* kw = two ? (pfw ? (const void*)k_rw<true, 2, true> : (const void*)k_rw<true, 2, false>)
-                           : nt == 128 ? (const void*)k_rw<false, 2, false> : (const void*)k_rw<false, 4, false>;
+      const uint32_t bs = (!two && nt == 256) ? 128u : 64u;
+      const void* kw = two ? (pfw ? (const void*)k_rw<true, 2, true, 1> : (const void*)k_rw<true, 2, false, 1>)
+                           : nt == 128 ? (const void*)k_rw<false, 2, false, 1> : (const void*)k_rw<false, 2, false, 2>;
       uint32_t grid = 0;
-      QDC_TRY(fused_grid(fg, kw, 64, grid));
+      QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
       fgeo g = fg;
       uint64_t tpb = 1;
       while (tpb * grid < g.ntiles) tpb <<= 1;
@@ -931,15 +932,15 @@ struct Circuit {
       if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
       last_fused_grid = grid;
       if (two && pfw)
-        return ctx.launch_block(name, bytes, k_rw<true, 2, true>, grid, 64u, f, b, fops, mats, g,
+        return ctx.launch_block(name, bytes, k_rw<true, 2, true, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
       if (two)
-        return ctx.launch_block(name, bytes, k_rw<true, 2, false>, grid, 64u, f, b, fops, mats, g,
+        return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
       if (nt == 128)
-        return ctx.launch_block(name, bytes, k_rw<false, 2, false>, grid, 64u, f, b, fops, mats, g,
+        return ctx.launch_block(name, bytes, k_rw<false, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
-      return ctx.launch_block(name, bytes, k_rw<false, 4, false>, grid, 64u, f, b, fops, mats, g,
+      return ctx.launch_block(name, bytes, k_rw<false, 2, false, 2>, grid, bs, f, b, fops, mats, g,
                               l0, partials, stride);
     }
     const void* kern = nullptr;

@@ -57,11 +57,16 @@ inline void qk_operands(const cx* U, std::vector<real>& a) {
       }
 }
 
-template <int K>
+// P = 2 (f32, qubit 0 not a target): lane j of quad q owns the adjacent groups 2j and 2j + 1,
+// whose amplitudes at each offset form one 16-B chunk — every load and store is 16 B per lane
+// (256 contiguous bytes per quad) and each batch runs the MFMA chain twice.  P = 1: one group
+// per lane, 8-B (f32) accesses.
+template <int K, int P>
 __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __restrict__ aop,
                                             qk_geo g) {
   constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
 #ifdef QDC_F64
+  static_assert(P == 1, "f64 amplitudes are 16 B already");
   using acc_t = double __attribute__((ext_vector_type(4)));
 #else
   using acc_t = float __attribute__((ext_vector_type(4)));
@@ -76,42 +81,67 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
   uint64_t off[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) off[m] = g.off[M * q + m];
-  // NB batches of 16 groups per iteration, all loads first (bytes in flight per wave)
-  constexpr int NB = K == 3 ? 4 : K == 4 ? 2 : 1;
-  const uint64_t nbatch = (g.ngroups + 15) / 16;
+  // NB batches of 16 P groups per iteration, all loads first (bytes in flight per wave)
+  constexpr int NB0 = K == 3 ? 4 : K == 4 ? 2 : 1;
+  constexpr int NB = NB0;
+  constexpr uint64_t GB = 16 * P;  // groups per batch
+  const uint64_t nbatch = (g.ngroups + GB - 1) / GB;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   for (uint64_t bt0 = wave * NB; bt0 < nbatch; bt0 += nwaves * NB) {
     uint64_t base[NB];
     bool live[NB];
-    cx x[NB][M];
+    cx x[NB][P][M];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
-      const uint64_t grp = (bt0 + nb) * 16 + (uint64_t)j;
-      live[nb] = grp < g.ngroups;
+      const uint64_t grp = (bt0 + nb) * GB + (uint64_t)j * P;
+      live[nb] = grp < g.ngroups;  // ngroups is even when P = 2 (k < n)
       base[nb] = grp;
 #pragma unroll
       for (int b = 0; b < K; ++b) base[nb] = insert_zero(base[nb], g.sorted[b]);
 #pragma unroll
-      for (int m = 0; m < M; ++m) x[nb][m] = live[nb] ? s[base[nb] + off[m]] : cx{0, 0};
+      for (int m = 0; m < M; ++m) {
+        if constexpr (P == 2) {
+          const chunk c = live[nb] ? ldc(reinterpret_cast<const chunk*>(s + base[nb] + off[m]))
+                                   : chunk{};
+          x[nb][0][m] = c.v[0];
+          x[nb][1][m] = c.v[1];
+        } else {
+          x[nb][0][m] = live[nb] ? s[base[nb] + off[m]] : cx{0, 0};
+        }
+      }
     }
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        acc_t d = {0, 0, 0, 0};
+        acc_t d[P];
 #pragma unroll
-        for (int u = 0; u < S; ++u) {
-          const real bv = (u & 1) ? x[nb][u >> 1].y : x[nb][u >> 1].x;
+        for (int p = 0; p < P; ++p) {
+          d[p] = acc_t{0, 0, 0, 0};
+#pragma unroll
+          for (int u = 0; u < S; ++u) {
+            const real bv = (u & 1) ? x[nb][p][u >> 1].y : x[nb][p][u >> 1].x;
 #ifdef QDC_F64
-          d = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][u], bv, d, 0, 0, 0);
+            d[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][u], bv, d[p], 0, 0, 0);
 #else
-          d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u], bv, d, 0, 0, 0);
+            d[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u], bv, d[p], 0, 0, 0);
 #endif
+          }
         }
         if (live[nb]) {
-          s[base[nb] + off[2 * t]] = cx{d[0], d[1]};
-          s[base[nb] + off[2 * t + 1]] = cx{d[2], d[3]};
+          if constexpr (P == 2) {
+            chunk c0, c1;
+            c0.v[0] = cx{d[0][0], d[0][1]};
+            c0.v[1] = cx{d[1][0], d[1][1]};
+            c1.v[0] = cx{d[0][2], d[0][3]};
+            c1.v[1] = cx{d[1][2], d[1][3]};
+            stc(reinterpret_cast<chunk*>(s + base[nb] + off[2 * t]), c0);
+            stc(reinterpret_cast<chunk*>(s + base[nb] + off[2 * t + 1]), c1);
+          } else {
+            s[base[nb] + off[2 * t]] = cx{d[0][0], d[0][1]};
+            s[base[nb] + off[2 * t + 1]] = cx{d[0][2], d[0][3]};
+          }
         }
       }
     }
@@ -183,16 +213,29 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   std::memcpy(ring.host[slot], a.data(), a.size() * sizeof(real));
   QDC_HIP(hipMemcpyAsync(ring.dev[slot], ring.host[slot], a.size() * sizeof(real),
                          hipMemcpyHostToDevice, c.stream));
-  const uint64_t nb = k == 3 ? 4 : k == 4 ? 2 : 1;  // batches per wave iteration (k_qk)
-  const uint64_t waves = ((g.ngroups + 15) / 16 + nb - 1) / nb;
+  // 16-B accesses (two adjacent groups per lane) when qubit 0 is not a target (f32); measured
+  // at n = 28 (tools/qk_probe.py): k = 3 +5-7 %, k = 5 +5 %, k = 4 -10 % (kept at 8 B)
+  bool pair = sizeof(real) == 4 && g.sorted[0] != 0 && k != 4;
+  if (const char* ev = getenv("QDC_QK_PAIR")) pair = pair && atoi(ev) != 0;
+  const uint64_t nb0 = k == 3 ? 4 : k == 4 ? 2 : 1;  // batches per wave iteration (k_qk)
+  const uint64_t nb = nb0;
+  const uint64_t gpb = pair ? 32 : 16;  // groups per batch
+  const uint64_t waves = ((g.ngroups + gpb - 1) / gpb + nb - 1) / nb;
   const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 256u * 16u);
   c.next_flops = 8.0 * C * (double)((uint64_t)1 << n);  // C complex MACs per amplitude
   const double bytes = 2.0 * state_bytes(n);
   const real* buf = ring.dev[slot];
   const char* e;
-  if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3>, grid, 256u, s, buf, g);
-  else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4>, grid, 256u, s, buf, g);
-  else e = c.launch_block("qk5", bytes, k_qk<5>, grid, 256u, s, buf, g);
+#ifndef QDC_F64
+  if (pair) {
+    if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3, 2>, grid, 256u, s, buf, g);
+    else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4, 2>, grid, 256u, s, buf, g);
+    else e = c.launch_block("qk5", bytes, k_qk<5, 2>, grid, 256u, s, buf, g);
+  } else
+#endif
+  if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3, 1>, grid, 256u, s, buf, g);
+  else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4, 1>, grid, 256u, s, buf, g);
+  else e = c.launch_block("qk5", bytes, k_qk<5, 1>, grid, 256u, s, buf, g);
   QDC_TRY(e);
   QDC_HIP(hipEventRecord(ring.done[slot], c.stream));
   return nullptr;

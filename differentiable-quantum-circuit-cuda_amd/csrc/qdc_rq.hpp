@@ -616,31 +616,34 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 //  * every Gamma stage accumulates NE times the amplitudes per lane before its one 64-lane
 //    reduce-scatter (the reduction's cost per amplitude divides by NE);
 //  * waves are independent: while one computes, another on the SIMD loads or stores.
-// Registers: R = 16 NE amplitudes per state and lane (two-state NE = 2: 128 VGPRs of tile;
-// one-state NE = 4: 128), so 2 waves/SIMD.
+// Registers: R = 16 NE amplitudes per state and lane (two-state NE = 2: 128 VGPRs of tile),
+// so 2 waves/SIMD.  One-state tiles (2^12 amplitudes) run on W = 2 waves with NE = 2 (a block
+// of 128 threads holds k_rq's thread bits 0..6; relayouts then take block barriers).
 #ifndef QDC_RW_WAVES
 #define QDC_RW_WAVES 2
 #endif
-template <bool TWO, int NE, bool PF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 1 : QDC_RW_WAVES, PF ? 1 : QDC_RW_WAVES)))
+template <bool TWO, int NE, bool PF, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PF ? 1 : QDC_RW_WAVES, PF ? 1 : QDC_RW_WAVES)))
 void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
   static_assert(NE == 2 || NE == 4, "k_rw: 2 or 4 register groups");
+  static_assert(W == 1 || (W == 2 && !TWO), "k_rw: two-state tiles are one wave");
   constexpr int LOGNE = NE == 2 ? 1 : 2;
+  constexpr int TB = W == 1 ? 6 : 7;  // k_rq thread bits held by the block's threads
   constexpr int R = RQ_R * NE;   // amplitudes per lane and state
   constexpr int CPT = R / VEC;   // chunks per lane and state
   constexpr int CPG = RQ_R / VEC;  // chunks per register group (8)
-  __shared__ cx buf[64 * R];
+  __shared__ cx buf[64 * W * R];
   __shared__ real accw[TWO ? FMAX_GRAD_RQ : 1][FACC];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x;  // the block's thread (W = 1: the lane)
   if constexpr (TWO) {
     for (uint32_t i = lane; i < FMAX_GRAD_RQ * FACC; i += 64) (&accw[0][0])[i] = 0;
   }
   const rqio* io = reinterpret_cast<const rqio*>(mats + l0 + sizeof(rq_layout) / sizeof(cx));
   uint64_t thr_ld = 0, thr_st = 0;  // this lane's chunk offsets in the load / store layout
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < TB; ++k) {
     if ((lane >> k) & 1u) {
       thr_ld += io->gv_ld[k];
       thr_st += io->gv_st[k];
@@ -672,7 +675,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     uint64_t o = 0;
 #pragma unroll
     for (int i = 0; i < LOGNE; ++i)
-      if ((e >> i) & 1) o += gv[6 + i];
+      if ((e >> i) & 1) o += gv[TB + i];
     return o;
   };
   auto load = [&](cx (&xf)[R], cx (&xb)[R], uint64_t base) __attribute__((always_inline)) {
@@ -727,23 +730,27 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
                       const rq_layout* Ln) __attribute__((always_inline)) {
     uint32_t tpb = tp * (uint32_t)sizeof(cx), tpnb = tpn * (uint32_t)sizeof(cx);
     asm volatile("" : "+v"(tpb), "+v"(tpnb));  // opaque: LLVM would refactor the shift out
+    if constexpr (W > 1) __syncthreads();  // the buffer's previous reads are done
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       uint32_t te = 0;
 #pragma unroll
-      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Lc->tv[6 + i] : 0u;
+      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Lc->tv[TB + i] : 0u;
 #pragma unroll
       for (int j = 0; j < RQ_R; ++j) {
         const uint32_t u = (te ^ Lc->rp[j]) * (uint32_t)sizeof(cx);
         *reinterpret_cast<cx*>(__builtin_assume_aligned(bufb + (tpb ^ u), 8)) = x[16 * e + j];
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (W > 1)
+      __syncthreads();
+    else
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       uint32_t te = 0;
 #pragma unroll
-      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Ln->tv[6 + i] : 0u;
+      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Ln->tv[TB + i] : 0u;
 #pragma unroll
       for (int j = 0; j < RQ_R; ++j) {
         const uint32_t u = (te ^ Ln->rp[j]) * (uint32_t)sizeof(cx);
@@ -772,7 +779,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       if (kind == FK_RELAYOUT) {
         const rq_layout* Lc = reinterpret_cast<const rq_layout*>(mats + lcur);
         const rq_layout* Ln = reinterpret_cast<const rq_layout*>(M);
-        const uint32_t tp = rq_tp<6>(Lc, lane), tpn = rq_tp<6>(Ln, lane);
+        const uint32_t tp = rq_tp<TB>(Lc, lane), tpn = rq_tp<TB>(Ln, lane);
         exchange(xf, tp, Lc, tpn, Ln);
         if constexpr (TWO) exchange(xb, tp, Lc, tpn, Ln);
         lcur = op.mat;

@@ -36,7 +36,7 @@ def bench_name(kernel):
         two, wf = m.group(1) == "true", m.group(3) == "true"
         return ("fused_reverse" if wf else "fused_inject") if two else \
                ("fused_apply" if wf else "fused_density")
-    m = re.search(r"k_r[qw]<(true|false), \d+(?:, (?:true|false))?>", kernel)
+    m = re.search(r"k_r[qw]<(true|false), \d+[^>]*>", kernel)
     if m:  # register-resident gate passes (qdc_rq.hpp): k_rq<TWO, NT, PF>, k_rw<TWO, NE, PF>
         return "fused_reverse" if m.group(1) == "true" else "fused_apply"
     if "k_elementwise<0>" in kernel:
