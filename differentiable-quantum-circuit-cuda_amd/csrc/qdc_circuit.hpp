@@ -224,6 +224,7 @@ struct Circuit {
   int rq_stats = 0;
   int rq_prefetch = 1;      // one-state register-resident passes prefetch the next tile (QDC_RQ_PF)
   int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
+  int rq64 = 1;  // f64 gate passes register-resident too (k_rw; QDC_RQ64)
   int rq_order = 0;  // register-resident tile order: 0 block-contiguous, 1 grid-strided (QDC_RQ_ORDER)
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
@@ -284,6 +285,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PF2")) rq_prefetch2 = atoi(e);
     if (const char* e = getenv("QDC_RW")) rq_wave = atoi(e);
     if (const char* e = getenv("QDC_RQ_ORDER")) rq_order = atoi(e);
+    if (const char* e = getenv("QDC_RQ64")) rq64 = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
@@ -514,7 +516,7 @@ struct Circuit {
     // gate-only passes permute their tile on the way out when they are register-resident
     // (single-device layout only: the sharded remap planner owns the layout there)
     P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
-    P.rq_grad = rq_grad32 && use_rq && sizeof(real) == 4;
+    P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
     return P;
   }
@@ -593,7 +595,9 @@ struct Circuit {
     // 12-cx layout descriptors (one per relayout, plus L0)
     const size_t nfops = 2 * nops + items.size();
     mats_off = ((nfops * sizeof(fop) + 255) / 256) * 256;
-    const size_t bytes = mats_off + (nops * 32 + nfops * 12 + items.size() * 32) * sizeof(cx);  // <= 2 R^2 = 32 per stage
+    // matrices <= 2 R^2 = 32 per stage; layouts <= 12 cx; one rqio per register-resident pass
+    const size_t bytes =
+        mats_off + (nops * 32 + nfops * 12 + items.size() * (sizeof(rqio) / sizeof(cx))) * sizeof(cx);
     if (bytes > prog_cap) {
       QDC_TRY(sync_all());
       for (auto& d : devs) {
@@ -778,7 +782,7 @@ struct Circuit {
         }
       }
       // register-resident pass: f32, gate stages only (no densities / injections)
-      bool rq = use_rq && sizeof(real) == 4 && it.writes_f;
+      bool rq = use_rq && (sizeof(real) == 4 || rq64) && it.writes_f;
       for (const fop& F : pf) rq = rq && (F.kind & 7u) <= FK_DIAG;
       it.rq = rq;
       if (!it.swaps.empty() && !rq)
@@ -973,9 +977,34 @@ struct Circuit {
 #undef QDC_RQ_LAUNCH
     return fail("no register-resident kernel launched");
 #else
-    (void)ctx; (void)name; (void)bytes; (void)fg; (void)two; (void)tbits; (void)l0; (void)f; (void)b;
-    (void)fops; (void)mats; (void)partials; (void)stride;
-    return fail("register-resident passes are f32 only");
+    // f64: 16 amplitudes (4 VGPRs each) per lane and state; two-state 2^10-amplitude tiles on one
+    // wave, one-state 2^11 on two
+    // (a reverse sweep's passes before the first injection are one-state on 2^10 tiles: one wave)
+    const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
+    if (!(two ? nt == 64 : (nt == 64 || nt == 128)))
+      return fail("no register-resident kernel for a %u-amplitude %s tile", 1u << tbits,
+                  two ? "two-state" : "one-state");
+    const void* kw = two        ? (const void*)k_rw<true, 1, false, 1>
+                     : nt == 64 ? (const void*)k_rw<false, 1, false, 1>
+                                : (const void*)k_rw<false, 1, false, 2>;
+    const uint32_t bs = nt;
+    uint32_t grid = 0;
+    QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
+    fgeo g = fg;
+    uint64_t tpb = 1;
+    while (tpb * grid < g.ntiles) tpb <<= 1;
+    g.tpb = (uint32_t)tpb;
+    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
+    last_fused_grid = grid;
+    if (two)
+      return ctx.launch_block(name, bytes, k_rw<true, 1, false, 1>, grid, bs, f, b, fops, mats, g, l0,
+                              partials, stride);
+    if (nt == 64)
+      return ctx.launch_block(name, bytes, k_rw<false, 1, false, 1>, grid, bs, f, b, fops, mats, g, l0,
+                              partials, stride);
+    return ctx.launch_block(name, bytes, k_rw<false, 1, false, 2>, grid, bs, f, b, fops, mats, g, l0,
+                            partials, stride);
 #endif
   }
   // one wave of resident blocks (occupancy query, cached per kernel), or QDC_FUSED_BLOCKS

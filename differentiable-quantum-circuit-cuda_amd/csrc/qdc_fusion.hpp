@@ -372,9 +372,11 @@ struct RqLayout {
     return -1;
   }
   bool holds(uint32_t q) const { return find(q) >= 0; }
-  // HBM layouts (load / store): slot 0 = tile bit 0 (a 16-B chunk is one thread's register
-  // pair) and tile bits 1..3 are thread bits 0..2 (lanes 0..7 read 128 contiguous bytes)
+  // HBM layouts (load / store), lanes 0..7 reading 128 contiguous bytes: f32 (LV = 1) slot 0 =
+  // tile bit 0 (a 16-B chunk is one thread's register pair) and tile bits 1..3 are thread bits
+  // 0..2; f64 (LV = 0, a chunk is one amplitude) tile bits 0..2 are thread bits 0..2
   bool hbm_ok() const {
+    if (LV == 0) return !holds(0) && !holds(1) && !holds(2);
     return slot[0] == 0 && !holds(1) && !holds(2) && !holds(3);
   }
 };
@@ -409,10 +411,12 @@ inline rq_layout rq_descriptor(const RqLayout& L, uint32_t T) {
 // the register chunk index (slots 1..3), with tile chunk bit c at global chunk bit
 // c (c < lc) or hb[c - lc].
 // dest (store of a permuting pass): tile bit q's value goes where tile bit dest[q] sits.
+// f32: register chunk i = register pair (2i, 2i + 1), its index bits slots 1..3; f64: register
+// chunk j = register j, index bits slots 0..3.
 inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* hb,
                    uint64_t* gv, uint64_t* offi, const uint32_t* dest = nullptr) {
-  auto gbit = [&](uint32_t tile_bit) -> uint64_t {  // tile bit >= 1 -> global chunk offset
-    const uint32_t c = (dest ? dest[tile_bit] : tile_bit) - 1;
+  auto gbit = [&](uint32_t tile_bit) -> uint64_t {  // tile bit >= LV -> global chunk offset
+    const uint32_t c = (dest ? dest[tile_bit] : tile_bit) - (uint32_t)LV;
     return 1ull << (c < lc ? c : hb[c - lc]);
   };
   uint32_t th[8];
@@ -420,10 +424,11 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
   uint32_t k = 0;
   for (; k < nt; ++k) gv[k] = gbit(th[k]);
   for (; k < 8; ++k) gv[k] = 0;
-  for (uint32_t i = 0; i < (uint32_t)RQ_R / 2; ++i) {
+  constexpr int S0 = LV;  // the first slot that is a chunk bit
+  for (uint32_t i = 0; i < ((uint32_t)RQ_R >> LV); ++i) {
     uint64_t o = 0;
-    for (int s = 1; s < 4; ++s)
-      if ((i >> (s - 1)) & 1u) o += gbit(L.slot[s]);
+    for (int s = S0; s < 4; ++s)
+      if ((i >> (s - S0)) & 1u) o += gbit(L.slot[s]);
     offi[i] = o;
   }
 }
@@ -451,7 +456,7 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
   auto fits = [&](const RqLayout& L, size_t j) {
     return L.holds(st[j].t1) && L.holds(st[j].t2);
   };
-  auto hbm_allowed = [](uint32_t q) { return q == 0 || q > 3; };
+  auto hbm_allowed = [](uint32_t q) { return LV == 0 ? q > 2 : (q == 0 || q > 3); };
   // the qubit set of a relayout: stage j0 first, then greedily the stages that become ready
   auto cover = [&](uint64_t done, size_t j0, std::vector<uint32_t> S, bool hbm) {
     auto add = [&](size_t j) {
@@ -492,10 +497,10 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
       if ((!hbm || hbm_allowed(q)) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
     return S;
   };
-  // slots for a qubit set: members of `prev` keep their slot, slot 0 = bit 0 if `hbm`
+  // slots for a qubit set: members of `prev` keep their slot, slot 0 = bit 0 if `hbm` (f32)
   auto place = [&](const std::vector<uint32_t>& S, const RqLayout& prev, bool hbm) {
     RqLayout L{{~0u, ~0u, ~0u, ~0u}};
-    if (hbm) L.slot[0] = 0;
+    if (hbm && LV == 1) L.slot[0] = 0;
     for (uint32_t q : S) {
       if (L.holds(q)) continue;
       const int ps = prev.find(q);
@@ -556,7 +561,8 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
   uint64_t done = 0;
   {  // load layout
     const RqLayout none{{~0u, ~0u, ~0u, ~0u}};
-    P.load = place(best_cover(0, {0u}, true), none, true);
+    P.load = place(best_cover(0, LV == 1 ? std::vector<uint32_t>{0u} : std::vector<uint32_t>{}, true),
+                   none, true);
   }
   RqLayout cur = P.load;
   for (size_t left = n; left > 0;) {
@@ -569,7 +575,7 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
       std::vector<uint32_t> S;
       bool hbm = false;
       if (!src && max_closure) {
-        S = best_cover(done, {0u}, true);
+        S = best_cover(done, LV == 1 ? std::vector<uint32_t>{0u} : std::vector<uint32_t>{}, true);
         hbm = closure(done, S) == (int)left;
       }
       if (!hbm) S = best_cover(done, {}, false);
@@ -604,9 +610,10 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
   } else if (cur.hbm_ok()) {
     P.store = cur;
   } else {
-    std::vector<uint32_t> S{0u};
+    std::vector<uint32_t> S;
+    if (LV == 1) S.push_back(0u);
     for (int s = 0; s < 4; ++s)
-      if (hbm_allowed(cur.slot[s]) && cur.slot[s] != 0) S.push_back(cur.slot[s]);
+      if (hbm_allowed(cur.slot[s]) && (LV == 0 || cur.slot[s] != 0)) S.push_back(cur.slot[s]);
     for (uint32_t q = T; q-- > 0 && S.size() < 4;)
       if (hbm_allowed(q) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
     P.store = place(S, cur, true);

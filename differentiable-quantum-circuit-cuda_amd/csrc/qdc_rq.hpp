@@ -46,11 +46,12 @@ static_assert(sizeof(rq_layout) == 96, "rq_layout is 12 complex of the program")
 // t (thread bit k's chunk offset) and offi[i] = the offset of register chunk bits i (slots 1..3).
 // The load layout (the pass's first) and the store layout (its last) may differ.
 struct rqio {
-  uint64_t gv_ld[8], offi_ld[RQ_R / 2], gv_st[8], offi_st[RQ_R / 2];
+  uint64_t gv_ld[8], offi_ld[RQ_R], gv_st[8], offi_st[RQ_R];  // offi: RQ_R / VEC chunks used
 };
-static_assert(sizeof(rqio) == 256, "rqio is 32 complex of the program");
+static_assert(sizeof(rqio) % sizeof(cx) == 0, "rqio is whole complex values of the program");
 
-#ifndef QDC_F64
+// Everything below builds in both precisions; k_rq and the prefetch loads are f32 only (never
+// instantiated by the f64 runtime), k_rw runs both.
 
 // fop.t1 of a register stage = slot case: two-qubit / diagonal: 2P + O for slot pair P with
 // t1 (the stage's low qubit) in slot 2P + O and t2 in the other slot of the pair; one-qubit: slot.
@@ -627,13 +628,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PF ? 1 :
 void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
-  static_assert(NE == 2 || NE == 4, "k_rw: 2 or 4 register groups");
+  static_assert(NE == 1 || NE == 2 || NE == 4, "k_rw: 1, 2 or 4 register groups");
   static_assert(W == 1 || (W == 2 && !TWO), "k_rw: two-state tiles are one wave");
-  constexpr int LOGNE = NE == 2 ? 1 : 2;
+  constexpr int LOGNE = NE == 1 ? 0 : NE == 2 ? 1 : 2;
   constexpr int TB = W == 1 ? 6 : 7;  // k_rq thread bits held by the block's threads
   constexpr int R = RQ_R * NE;   // amplitudes per lane and state
   constexpr int CPT = R / VEC;   // chunks per lane and state
-  constexpr int CPG = RQ_R / VEC;  // chunks per register group (8)
+  constexpr int CPG = RQ_R / VEC;  // chunks per register group (f32 8, f64 16)
   __shared__ cx buf[64 * W * R];
   __shared__ real accw[TWO ? FMAX_GRAD_RQ : 1][FACC];
   const uint32_t lane = threadIdx.x;  // the block's thread (W = 1: the lane)
@@ -688,12 +689,12 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #pragma unroll
       for (int i = 0; i < CPG; ++i) {
         const chunk cf = ldc(pf + (eo + rg->offi_ld[i]));
-        xf[16 * e + 2 * i] = cf.v[0];
-        xf[16 * e + 2 * i + 1] = cf.v[1];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) xf[16 * e + VEC * i + v] = cf.v[v];
         if constexpr (TWO) {
           const chunk cb = ldc(pb + (eo + rg->offi_ld[i]));
-          xb[16 * e + 2 * i] = cb.v[0];
-          xb[16 * e + 2 * i + 1] = cb.v[1];
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) xb[16 * e + VEC * i + v] = cb.v[v];
         }
       }
     }
@@ -709,12 +710,12 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #pragma unroll
       for (int i = 0; i < CPG; ++i) {
         chunk c;
-        c.v[0] = xf[16 * e + 2 * i];
-        c.v[1] = xf[16 * e + 2 * i + 1];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) c.v[v] = xf[16 * e + VEC * i + v];
         stc(pf + (eo + rg->offi_st[i]), c);
         if constexpr (TWO) {
-          c.v[0] = xb[16 * e + 2 * i];
-          c.v[1] = xb[16 * e + 2 * i + 1];
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) c.v[v] = xb[16 * e + VEC * i + v];
           stc(pb + (eo + rg->offi_st[i]), c);
         }
       }
@@ -855,6 +856,5 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     }
   }
 }
-#endif
 
 }  // namespace qdc

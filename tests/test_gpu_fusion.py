@@ -237,3 +237,32 @@ def test_permuting_passes_equal_fixed_layout(n, perm_low):
         fl.check("grads", g, what)
         fl.check("state", fs, what)
         fl.check("uncomputed", us, what)
+
+
+@pytest.mark.parametrize("case", ["layered12", "random12", "random15"])
+def test_f64_register_resident_passes_equal_lds_passes(case):
+    """f64 gate passes run register-resident too (k_rw: one wave per 2^10-amplitude two-state
+    tile, four VGPRs per amplitude, HBM layouts with tile bits 0..2 as thread bits since a
+    16-B chunk is one amplitude).  QDC_RQ64=0 keeps them on the LDS tiles; both agree with the
+    oracle within 4x the f64 floor and with each other."""
+    kind, n = case[:-2], int(case[-2:])
+    if kind == "layered":
+        ins, var = O.layered_circuit(n, 4, seed=25)
+        const, psi0 = [], None
+    else:
+        ins, const, var = O.random_circuit(n, 160, seed=300 + n, density_every=0)
+        psi0 = O.random_state(np.random.default_rng(n + 1), n)
+    fl = F.Floor("f64", n, ins, const, var, psi0=psi0, run=False)
+    res = {}
+    for rq64 in (1, 0):
+        c = build_env("f64", n, ins, {"QDC_RQ64": rq64, "QDC_FUSE": 1})
+        if psi0 is not None:
+            c.set_state_from_vector(fl.psi0)
+        d = c.forward(fl.const, fl.var)
+        g = c.backward(fl.cots, fl.const, fl.var)
+        what = f"{case} f64 QDC_RQ64={rq64} "
+        fl.check("forward", d, what)
+        fl.check("grads", g, what)
+        fl.check("uncomputed", c.get_state(0), what)
+        res[rq64] = g
+    F.check_pair("f64", res[1], res[0], fl.floor["grads"], f"{case} f64 k_rw vs lds grads")

@@ -2,8 +2,9 @@
 planner, csrc/qdc_fusion.hpp rq_plan) on CPU.
 
 A plan is valid when, replayed step by step:
-  * the load and store layouts are HBM layouts (slot 0 = tile bit 0, tile bits 1..3 are thread
-    bits), and every layout holds 4 distinct tile bits;
+  * the load and store layouts are HBM layouts (f32: slot 0 = tile bit 0, tile bits 1..3 are
+    thread bits; f64, a 16-B chunk per amplitude: tile bits 0..2 are thread bits), and every
+    layout holds 4 distinct tile bits;
   * every stage runs exactly once, after the stages it depends on;
   * a stage runs on the current layout with its qubits in the slots its slot case names
     (one-qubit: the slot of t1; two-qubit / diagonal: 4 * slot(t1) + slot(t2)).
@@ -34,10 +35,12 @@ def random_pass(rng, T, nst, brick=False):
     return stages, deps
 
 
-def check_plan(T, stages, deps, plan):
+def check_plan(T, stages, deps, plan, prec="f32"):
     load, steps, store = plan
 
     def hbm_ok(L):
+        if prec == "f64":
+            return not ({0, 1, 2} & set(L))
         return L[0] == 0 and not ({1, 2, 3} & set(L))
 
     assert hbm_ok(load) and hbm_ok(store), (load, store)
@@ -62,9 +65,9 @@ def check_plan(T, stages, deps, plan):
     return relayouts
 
 
-@pytest.mark.parametrize("T", [11, 12])
+@pytest.mark.parametrize("prec,T", [("f32", 11), ("f32", 12), ("f64", 10), ("f64", 11)])
 @pytest.mark.parametrize("brick", [False, True])
-def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, T, brick):
+def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, prec, T, brick):
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(T * 2 + brick)
     total = {"1": 0, "0": 0}
@@ -72,5 +75,6 @@ def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, T, brick):
         stages, deps = random_pass(rng, T, int(rng.integers(1, 40)), brick)
         for mc in ("1", "0"):
             monkeypatch.setenv("QDC_RQ_MAXCL", mc)
-            total[mc] += check_plan(T, stages, deps, q.rq_plan(T, stages, deps, precision="f32"))
+            total[mc] += check_plan(T, stages, deps, q.rq_plan(T, stages, deps, precision=prec),
+                                    prec)
     assert total["1"] <= total["0"], total
