@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 typedef float vec4 __attribute__((ext_vector_type(4)));
@@ -228,6 +229,30 @@ int main(int argc, char** argv) {
       const float ms = timeit(e0, e1, launch, &r, 5);
       printf("stream rmw ns=%d U=%d             %7.3f ms  %6.2f TB/s\n", ns, u, ms, 2 * ns * S / ms / 1e9);
     }
+  if (argc > 1 && strcmp(argv[1], "pad") == 0) {
+    // two states in one allocation, b = f + S + pad: does the relative placement of the two
+    // streams matter?
+    vec4* base;
+    const size_t maxpad = (size_t)64 << 20;
+    CK(hipMalloc(&base, 2 * nch * 16 + maxpad));
+    CK(hipMemset(base, 0, 2 * nch * 16 + maxpad));
+    const size_t pads[] = {0, 256, 1024, 4096, 16384, 65536, 262144, (size_t)1 << 20,
+                           ((size_t)1 << 21) + 4096, ((size_t)32 << 20) + 8192};
+    for (size_t pad : pads) {
+      r.f = base;
+      r.b = base + (nch * 16 + pad) / 16;
+      r.mode = 1;
+      r.ns = 2;
+      r.u = 8;
+      r.grid = cus * 8;
+      float best = 1e9f;
+      for (int rep = 0; rep < 3; ++rep) best = std::min(best, timeit(e0, e1, launch, &r, 5));
+      printf("stream rmw ns=2 U=8 pad %10zu B %7.3f ms  %6.2f TB/s\n", pad, best, 4 * S / best / 1e9);
+    }
+    r.f = f;
+    r.b = b;
+    return 0;
+  }
   // tile patterns: rows = list of chunk bit positions (after lc)
   struct Pat {
     const char* name;
