@@ -359,21 +359,23 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   return items.size();
 }
 
-QDC_API size_t qdc_rq_plan(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
-                           const unsigned* t2, const unsigned long long* deps, size_t n,
-                           unsigned* steps, size_t cap) {
+QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds,
+                           const unsigned* t1, const unsigned* t2,
+                           const unsigned long long* deps, size_t n, unsigned* steps,
+                           size_t cap) {
   if (n > 64) return SIZE_MAX;  // rq_plan's stage sets are 64-bit masks (passes hold <= FMAX_OPS)
+  if (slots != 4 && slots != 5) return SIZE_MAX;
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
   const char* mc = getenv("QDC_RQ_MAXCL");  // the runtime's knob (qdc_circuit.hpp)
-  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, !(mc && atoi(mc) == 0));
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, !(mc && atoi(mc) == 0), slots);
   if (plan.steps.size() + 2 > cap) return SIZE_MAX;
   auto put = [&](size_t i, unsigned kind, unsigned stage, unsigned cs, const qdc::RqLayout& L) {
-    unsigned* o = steps + 7 * i;
+    unsigned* o = steps + 8 * i;
     o[0] = kind;
     o[1] = stage;
     o[2] = cs;
-    for (int s = 0; s < 4; ++s) o[3 + s] = L.slot[s];
+    for (int s = 0; s < qdc::RQ_SLOTS_MAX; ++s) o[3 + s] = (unsigned)s < L.ns ? L.slot[s] : ~0u;
   };
   put(0, 2u, 0u, 0u, plan.load);
   for (size_t i = 0; i < plan.steps.size(); ++i)

@@ -225,6 +225,8 @@ struct Circuit {
   int rq_prefetch = 1;      // one-state register-resident passes prefetch the next tile (QDC_RQ_PF)
   int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
   int rq64 = 1;  // f64 gate passes register-resident too (k_rw; QDC_RQ64)
+  int rq_slots5 = 1;  // two-state f32 k_rw passes plan five register slots (QDC_RQ_SLOTS5)
+  bool rq5() const { return rq_slots5 != 0 && (rq_wave & 1) && !(rq_wave & 4); }
   int rq_order = 0;  // register-resident tile order: 0 block-contiguous, 1 grid-strided (QDC_RQ_ORDER)
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
@@ -286,6 +288,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RW")) rq_wave = atoi(e);
     if (const char* e = getenv("QDC_RQ_ORDER")) rq_order = atoi(e);
     if (const char* e = getenv("QDC_RQ64")) rq64 = atoi(e);
+    if (const char* e = getenv("QDC_RQ_SLOTS5")) rq_slots5 = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
@@ -506,6 +509,7 @@ struct Circuit {
     bool writes_f = false;     // gate stages (fwd changes; else fwd is only read)
     std::vector<uint32_t> grad_slots;  // reduction slot of each reduction op, in op order
     bool rq = false;   // register-resident pass (qdc_rq.hpp): k_rq, ops include relayouts
+    bool s5 = false;   // rq with five register slots (k_rw<true, 2, false, 1, true>)
     uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
     uint32_t tbits = 0;  // amplitude bits of the tile
   };
@@ -597,7 +601,9 @@ struct Circuit {
     mats_off = ((nfops * sizeof(fop) + 255) / 256) * 256;
     // matrices <= 2 R^2 = 32 per stage; layouts <= 12 cx; one rqio per register-resident pass
     const size_t bytes =
-        mats_off + (nops * 32 + nfops * 12 + items.size() * (sizeof(rqio) / sizeof(cx))) * sizeof(cx);
+        mats_off + (nops * 32 + nfops * (sizeof(rq_layout) / sizeof(cx)) +
+                    items.size() * (sizeof(rqio) / sizeof(cx))) *
+                       sizeof(cx);
     if (bytes > prog_cap) {
       QDC_TRY(sync_all());
       for (auto& d : devs) {
@@ -832,7 +838,10 @@ struct Circuit {
           if (dest[t] < 4) src[dest[t]] = t;
         }
       }
-      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0);
+      // five register slots on the one-wave two-state f32 kernel (k_rw<.., S5>)
+      const uint32_t ns = (sizeof(real) == 4 && two && rq5()) ? 5u : 4u;
+      it.s5 = ns == 5;
+      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
       it.l0 = put_layout(P.load);
       {  // rqio after the load descriptor
         rqio io{};
@@ -858,8 +867,8 @@ struct Circuit {
           // cases): exchange t1 and t2 by permuting the matrices' index bits, and the
           // stage's Gamma back on the host
           const uint32_t kd = F.kind & 7u;
-          if ((kd == FK_Q2 || kd == FK_DIAG) && (step.cs >> 2) > (step.cs & 3u)) {
-            F.t1 = (step.cs & 3u) * 4u + (step.cs >> 2);
+          if ((kd == FK_Q2 || kd == FK_DIAG) && (step.cs >> 3) > (step.cs & 7u)) {
+            F.t1 = (step.cs & 7u) * 8u + (step.cs >> 3);
             const int nm = kd == FK_DIAG ? 4 : 16;
             for (int h = 0; h < 2; ++h) {  // A, then B
               cx* m = &mats[F.mat + (size_t)h * nm];
@@ -879,6 +888,12 @@ struct Circuit {
       }
       it.nstage = n;
       if (rq_stats) fprintf(stderr, "rq pass: %zu stages, %u ops (T=%u lc=%u)\n", pf.size(), n, it.tbits, it.lc);
+      if (rq_stats >= 2) {  // the pass's stages for offline planner studies (tools/)
+        fprintf(stderr, "rq stages %s T=%u perm=%d:", two ? "two" : "one", it.tbits, perm ? 1 : 0);
+        for (const RqStage& r : rs)
+          fprintf(stderr, " %u,%u,%u,%llx", r.kind, r.t1, r.t2, (unsigned long long)r.deps);
+        fprintf(stderr, "\n");
+      }
     }
     for (auto& d : devs) {  // prog_host is not rewritten before the call's final sync
       QDC_TRY(d->ctx.use());
@@ -917,14 +932,17 @@ struct Circuit {
   // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
   const char* launch_rq(Ctx& ctx, const char* name, double bytes, const fgeo& fg, bool two,
                         uint32_t tbits, uint32_t l0, chunk* f, chunk* b, const fop* fops,
-                        const cx* mats, cx* partials, uint64_t stride) {
+                        const cx* mats, cx* partials, uint64_t stride, bool s5) {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
       // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);
       const uint32_t bs = (!two && nt == 256) ? 128u : 64u;
-      const void* kw = two ? (pfw ? (const void*)k_rw<true, 2, true, 1> : (const void*)k_rw<true, 2, false, 1>)
+      if (s5 && !(two && !pfw)) return fail("internal: a five-slot pass without its kernel");
+      const void* kw = two ? (pfw  ? (const void*)k_rw<true, 2, true, 1>
+                              : s5 ? (const void*)k_rw<true, 2, false, 1, true>
+                                   : (const void*)k_rw<true, 2, false, 1>)
                            : nt == 128 ? (const void*)k_rw<false, 2, false, 1> : (const void*)k_rw<false, 2, false, 2>;
       uint32_t grid = 0;
       QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
@@ -938,6 +956,9 @@ struct Circuit {
       if (two && pfw)
         return ctx.launch_block(name, bytes, k_rw<true, 2, true, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
+      if (two && s5)
+        return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1, true>, grid, bs, f, b, fops,
+                                mats, g, l0, partials, stride);
       if (two)
         return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
@@ -1066,7 +1087,8 @@ struct Circuit {
       const uint64_t stride = (uint64_t)NBMAX * RED;
       ctx.next_flops = flops;
       if (it.rq) {
-        QDC_TRY(launch_rq(ctx, name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride));
+        QDC_TRY(launch_rq(ctx, name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride,
+                          it.s5));
       } else if (two) {
         if (it.writes_f)
           QDC_TRY((launch_fused<true, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));

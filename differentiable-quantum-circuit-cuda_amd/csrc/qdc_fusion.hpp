@@ -342,19 +342,27 @@ struct RqStage {
   uint32_t kind, t1, t2;
   uint64_t deps = 0;
 };
+constexpr int RQ_SLOTS_MAX = 5;  // register slots of a layout: 4, or 5 (k_rw two-state f32)
 struct RqLayout {
-  uint32_t slot[4];  // tile bit held by register slot s
+  uint32_t ns = 4;  // register slots (register index bits 0..ns-1)
+  uint32_t slot[RQ_SLOTS_MAX] = {~0u, ~0u, ~0u, ~0u, ~0u};  // tile bit held by register slot s
   // thread bits: the tile bits not in a slot, ascending — or, with tfix, tfirst[0..2] first
   // (a permuting pass's store layout: the bits that land on chunk bits 0..2)
   bool tfix = false;
   uint32_t tfirst[3] = {0, 0, 0};
-  bool operator==(const RqLayout& o) const {
-    return slot[0] == o.slot[0] && slot[1] == o.slot[1] && slot[2] == o.slot[2] &&
-           slot[3] == o.slot[3] && tfix == o.tfix &&
-           (!tfix || (tfirst[0] == o.tfirst[0] && tfirst[1] == o.tfirst[1] &&
-                      tfirst[2] == o.tfirst[2]));
+  static RqLayout empty(uint32_t ns) {
+    RqLayout L;
+    L.ns = ns;
+    return L;
   }
-  // the thread bits in order (k < T - 4)
+  bool operator==(const RqLayout& o) const {
+    if (ns != o.ns || tfix != o.tfix) return false;
+    for (uint32_t s = 0; s < ns; ++s)
+      if (slot[s] != o.slot[s]) return false;
+    return !tfix || (tfirst[0] == o.tfirst[0] && tfirst[1] == o.tfirst[1] &&
+                     tfirst[2] == o.tfirst[2]);
+  }
+  // the thread bits in order (k < T - ns)
   uint32_t threads(uint32_t T, uint32_t* out) const {
     uint32_t k = 0;
     if (tfix)
@@ -367,8 +375,8 @@ struct RqLayout {
     return k;
   }
   int find(uint32_t q) const {
-    for (int s = 0; s < 4; ++s)
-      if (slot[s] == q) return s;
+    for (uint32_t s = 0; s < ns; ++s)
+      if (slot[s] == q) return (int)s;
     return -1;
   }
   bool holds(uint32_t q) const { return find(q) >= 0; }
@@ -381,7 +389,7 @@ struct RqLayout {
   }
 };
 // One step of a planned pass: a relayout to L, or stage `stage` run with slot case `cs`
-// (qdc_rq.hpp: S1 * 4 + S2 for two-qubit / diagonal stages, the slot for one-qubit ones).
+// (qdc_rq.hpp: S1 * 8 + S2 for two-qubit / diagonal stages, the slot for one-qubit ones).
 struct RqStep {
   bool relayout;
   RqLayout L;
@@ -396,9 +404,9 @@ struct RqPlan {
 // tv[k] = swz(1 << k-th thread bit), thread bits = tile bits not in a slot, ascending.
 inline rq_layout rq_descriptor(const RqLayout& L, uint32_t T) {
   rq_layout d{};
-  for (uint32_t j = 0; j < (uint32_t)RQ_R; ++j) {
+  for (uint32_t j = 0; j < (1u << L.ns); ++j) {
     uint32_t idx = 0;
-    for (int s = 0; s < 4; ++s)
+    for (uint32_t s = 0; s < L.ns; ++s)
       if ((j >> s) & 1u) idx |= 1u << L.slot[s];
     d.rp[j] = swz(idx);
   }
@@ -424,10 +432,10 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
   uint32_t k = 0;
   for (; k < nt; ++k) gv[k] = gbit(th[k]);
   for (; k < 8; ++k) gv[k] = 0;
-  constexpr int S0 = LV;  // the first slot that is a chunk bit
-  for (uint32_t i = 0; i < ((uint32_t)RQ_R >> LV); ++i) {
+  constexpr uint32_t S0 = LV;  // the first slot that is a chunk bit
+  for (uint32_t i = 0; i < ((1u << L.ns) >> LV); ++i) {
     uint64_t o = 0;
-    for (int s = S0; s < 4; ++s)
+    for (uint32_t s = S0; s < L.ns; ++s)
       if ((i >> (s - S0)) & 1u) o += gbit(L.slot[s]);
     offi[i] = o;
   }
@@ -446,7 +454,7 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
 // a permuting pass (src != nullptr: src[b] = the tile bit whose value lands on tile bit b,
 // b < 4) the layout with slot 0 = src[0] and thread bits 0..2 = src[1..3].
 inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
-                      const uint32_t* src = nullptr, bool max_closure = true) {
+                      const uint32_t* src = nullptr, bool max_closure = true, uint32_t ns = 4) {
   const size_t n = st.size();
   auto qset = [&](size_t j, uint32_t* q) -> int {
     q[0] = st[j].t1;
@@ -467,7 +475,7 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
         if (hbm && !hbm_allowed(q[i])) return false;
         if (std::find(T2.begin(), T2.end(), q[i]) == T2.end()) T2.push_back(q[i]);
       }
-      if (T2.size() > 4) return false;
+      if (T2.size() > ns) return false;
       S = T2;
       return true;
     };
@@ -485,21 +493,21 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
       }
     }
     // fill: qubits of the next stages in index order, then the lowest allowed bits
-    for (size_t c = 0; c < n && S.size() < 4; ++c) {
+    for (size_t c = 0; c < n && S.size() < ns; ++c) {
       if ((sim >> c) & 1ull) continue;
       uint32_t q[2];
       const int m = qset(c, q);
-      for (int i = 0; i < m && S.size() < 4; ++i)
+      for (int i = 0; i < m && S.size() < ns; ++i)
         if ((!hbm || hbm_allowed(q[i])) && std::find(S.begin(), S.end(), q[i]) == S.end())
           S.push_back(q[i]);
     }
-    for (uint32_t q = T; q-- > 0 && S.size() < 4;)
+    for (uint32_t q = T; q-- > 0 && S.size() < ns;)
       if ((!hbm || hbm_allowed(q)) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
     return S;
   };
   // slots for a qubit set: members of `prev` keep their slot, slot 0 = bit 0 if `hbm` (f32)
   auto place = [&](const std::vector<uint32_t>& S, const RqLayout& prev, bool hbm) {
-    RqLayout L{{~0u, ~0u, ~0u, ~0u}};
+    RqLayout L = RqLayout::empty(ns);
     if (hbm && LV == 1) L.slot[0] = 0;
     for (uint32_t q : S) {
       if (L.holds(q)) continue;
@@ -508,7 +516,7 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
     }
     for (uint32_t q : S) {
       if (L.holds(q)) continue;
-      for (int s = 0; s < 4; ++s)
+      for (uint32_t s = 0; s < ns; ++s)
         if (L.slot[s] == ~0u) {
           L.slot[s] = q;
           break;
@@ -560,7 +568,7 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
   RqPlan P;
   uint64_t done = 0;
   {  // load layout
-    const RqLayout none{{~0u, ~0u, ~0u, ~0u}};
+    const RqLayout none = RqLayout::empty(ns);
     P.load = place(best_cover(0, LV == 1 ? std::vector<uint32_t>{0u} : std::vector<uint32_t>{}, true),
                    none, true);
   }
@@ -586,13 +594,14 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
     }
     const RqStage& s = st[pick];
     const uint32_t cs = s.kind == FK_Q1 ? (uint32_t)cur.find(s.t1)
-                                        : (uint32_t)(cur.find(s.t1) * 4 + cur.find(s.t2));
+                                        : (uint32_t)(cur.find(s.t1) * 8 + cur.find(s.t2));
     P.steps.push_back(RqStep{false, cur, (uint32_t)pick, cs});
     done |= 1ull << pick;
     --left;
   }
   if (src) {
-    RqLayout L{{src[0], ~0u, ~0u, ~0u}};
+    RqLayout L = RqLayout::empty(ns);
+    L.slot[0] = src[0];
     L.tfix = true;
     for (int i = 0; i < 3; ++i) L.tfirst[i] = src[1 + i];
     auto taken = [&](uint32_t q) {
@@ -600,9 +609,9 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
         if (src[i] == q) return true;
       return L.holds(q);
     };
-    for (int s = 1; s < 4; ++s)  // keep the current slots' qubits where possible
+    for (uint32_t s = 1; s < ns; ++s)  // keep the current slots' qubits where possible
       if (cur.slot[s] != ~0u && !taken(cur.slot[s])) L.slot[s] = cur.slot[s];
-    for (int s = 1; s < 4; ++s)
+    for (uint32_t s = 1; s < ns; ++s)
       for (uint32_t q = T; L.slot[s] == ~0u && q-- > 0;)
         if (!taken(q)) L.slot[s] = q;
     P.store = L;
@@ -612,9 +621,9 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
   } else {
     std::vector<uint32_t> S;
     if (LV == 1) S.push_back(0u);
-    for (int s = 0; s < 4; ++s)
+    for (uint32_t s = 0; s < ns; ++s)
       if (hbm_allowed(cur.slot[s]) && (LV == 0 || cur.slot[s] != 0)) S.push_back(cur.slot[s]);
-    for (uint32_t q = T; q-- > 0 && S.size() < 4;)
+    for (uint32_t q = T; q-- > 0 && S.size() < ns;)
       if (hbm_allowed(q) && std::find(S.begin(), S.end(), q) == S.end()) S.push_back(q);
     P.store = place(S, cur, true);
     P.steps.push_back(RqStep{true, P.store, 0, 0});

@@ -33,12 +33,14 @@ constexpr uint32_t FK_RELAYOUT = 7;
 constexpr int RQ_NT_ONE = 256;  // threads per one-state tile: 2^12 amplitudes = TILE_CHUNKS_1
 constexpr int RQ_NT_TWO = 128;  // threads per two-state tile: 2^11 amplitudes = TILE_CHUNKS_2
 
-// a register layout in the program's matrix area (12 cx = 96 B)
+// a register layout in the program's matrix area (160 B: 20 cx in f32, 10 in f64); 4-slot
+// layouts use rp[0..15], 5-slot ones (k_rw two-state f32) rp[0..31]
 struct rq_layout {
-  uint32_t rp[RQ_R];  // swz(dep(j -> slots)), in cx units
-  uint32_t tv[8];     // swz(1 << thread bit k), in cx units (k < log2 NT)
+  uint32_t rp[2 * RQ_R];  // swz(dep(j -> slots)), in cx units
+  uint32_t tv[8];         // swz(1 << thread bit k), in cx units (k < log2 NT)
 };
-static_assert(sizeof(rq_layout) == 96, "rq_layout is 12 complex of the program");
+static_assert(sizeof(rq_layout) == 160 && sizeof(rq_layout) % sizeof(cx) == 0,
+              "rq_layout is whole complex values of the program");
 
 // HBM addressing of a tile's registers (after the load layout's descriptor in the program).
 // Register pair (2i, 2i+1) of thread t is one 16-B chunk (slot 0 = tile bit 0); its chunk
@@ -53,8 +55,7 @@ static_assert(sizeof(rqio) % sizeof(cx) == 0, "rqio is whole complex values of t
 // Everything below builds in both precisions; k_rq and the prefetch loads are f32 only (never
 // instantiated by the f64 runtime), k_rw runs both.
 
-// fop.t1 of a register stage = slot case: two-qubit / diagonal: 2P + O for slot pair P with
-// t1 (the stage's low qubit) in slot 2P + O and t2 in the other slot of the pair; one-qubit: slot.
+// fop.t1 of a register stage = slot case (rq_stage); register index bit s = slot s.
 template <int S1, int S2>
 __device__ __forceinline__ constexpr int rq_el(int base, int r) {
   return base | ((r & 1) << S1) | ((r >> 1) << S2);
@@ -62,12 +63,12 @@ __device__ __forceinline__ constexpr int rq_el(int base, int r) {
 template <int S1, int S2>
 __device__ __forceinline__ constexpr int rq_base(int k) {  // k-th index with bits S1, S2 zero
   int b = 0, bit = 0;
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < 8; ++s) {  // the register index bits other than S1, S2, ascending
     if (s == S1 || s == S2) continue;
     if ((k >> bit) & 1) b |= 1 << s;
     ++bit;
   }
-  return b | ((k >> 2) << 4);  // registers beyond 16 (k_rw): bits above the four slots
+  return b;
 }
 
 // two-qubit stage on registers: f <- A f [, Gamma += b0 f0^T, b <- B b]
@@ -215,30 +216,32 @@ __device__ __forceinline__ void rq_q1(cx (&f)[R], cx (&b)[R], const cx* __restri
   }
 }
 
-// one register stage: slot case (host: rq_plan) two-qubit / diagonal S1 * 4 + S2 (t1 in slot
+// one register stage: slot case (host: rq_plan) two-qubit / diagonal S1 * 8 + S2 (t1 in slot
 // S1, t2 in slot S2, always S1 < S2: build_program exchanges t1 and t2 otherwise); one-qubit:
 // the slot of t1
 template <bool TWO, int R>
 __device__ __forceinline__ void rq_stage(uint32_t sel, cx (&xf)[R], cx (&xb)[R],
                                          const cx* __restrict__ M, bool gamma, real* acc) {
+  // slot 4 exists only with 32 registers (five-slot layouts)
+#define QDC_RQ_Q2(S1, S2)                                                             \
+  case FK_Q2 * 64 + (S1) * 8 + (S2):                                                  \
+    if constexpr ((S2) < 4 || R >= 32) rq_q2<S1, S2, TWO, R>(xf, xb, M, gamma, acc);   \
+    break;                                                                            \
+  case FK_DIAG * 64 + (S1) * 8 + (S2):                                                \
+    if constexpr ((S2) < 4 || R >= 32) rq_diag<S1, S2, TWO, R>(xf, xb, M, gamma, acc); \
+    break;
   switch (sel) {
-    case FK_Q2 * 16 + 1: rq_q2<0, 1, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q2 * 16 + 2: rq_q2<0, 2, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q2 * 16 + 3: rq_q2<0, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q2 * 16 + 6: rq_q2<1, 2, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q2 * 16 + 7: rq_q2<1, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q2 * 16 + 11: rq_q2<2, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 1: rq_diag<0, 1, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 2: rq_diag<0, 2, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 3: rq_diag<0, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 6: rq_diag<1, 2, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 7: rq_diag<1, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_DIAG * 16 + 11: rq_diag<2, 3, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q1 * 16 + 0: rq_q1<0, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q1 * 16 + 1: rq_q1<1, TWO, R>(xf, xb, M, gamma, acc); break;
-    case FK_Q1 * 16 + 2: rq_q1<2, TWO, R>(xf, xb, M, gamma, acc); break;
+    QDC_RQ_Q2(0, 1) QDC_RQ_Q2(0, 2) QDC_RQ_Q2(0, 3) QDC_RQ_Q2(1, 2) QDC_RQ_Q2(1, 3)
+    QDC_RQ_Q2(2, 3) QDC_RQ_Q2(0, 4) QDC_RQ_Q2(1, 4) QDC_RQ_Q2(2, 4) QDC_RQ_Q2(3, 4)
+    case FK_Q1 * 64 + 0: rq_q1<0, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 64 + 1: rq_q1<1, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 64 + 2: rq_q1<2, TWO, R>(xf, xb, M, gamma, acc); break;
+    case FK_Q1 * 64 + 4:
+      if constexpr (R >= 32) rq_q1<4, TWO, R>(xf, xb, M, gamma, acc);
+      break;
     default: rq_q1<3, TWO, R>(xf, xb, M, gamma, acc); break;
   }
+#undef QDC_RQ_Q2
 }
 
 // per-thread part of a layout's LDS index
@@ -528,7 +531,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         lcur = op.mat;
         continue;
       }
-      rq_stage<TWO>(kind * 16u + op.t1, xf, xb, M, gamma, acc);
+      rq_stage<TWO>(kind * 64u + op.t1, xf, xb, M, gamma, acc);
       if (gamma) ++ri;
     }
   };
@@ -623,12 +626,16 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #ifndef QDC_RW_WAVES
 #define QDC_RW_WAVES 2
 #endif
-template <bool TWO, int NE, bool PF, int W>
+// S5: five-slot layouts (NE = 2, W = 1): the register-group bit is register slot 4, which
+// stages address like the other four, so covers hold 5 qubits (fewer relayouts); the layout
+// descriptor then spans all 32 registers (rp[16 e + j], chunk offsets offi[8 e + i]).
+template <bool TWO, int NE, bool PF, int W, bool S5 = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PF ? 1 : QDC_RW_WAVES, PF ? 1 : QDC_RW_WAVES)))
 void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
   static_assert(NE == 1 || NE == 2 || NE == 4, "k_rw: 1, 2 or 4 register groups");
+  static_assert(!S5 || (NE == 2 && W == 1 && VEC == 2 && !PF), "five slots: f32 one-wave tiles");
   static_assert(W == 1 || (W == 2 && !TWO), "k_rw: two-state tiles are one wave");
   constexpr int LOGNE = NE == 1 ? 0 : NE == 2 ? 1 : 2;
   constexpr int TB = W == 1 ? 6 : 7;  // k_rq thread bits held by the block's threads
@@ -674,6 +681,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   // register group e (k_rq's thread bits 6.. = e): chunk offset sum of gv[6 + i] over e's bits
   auto goff = [&](const uint64_t* gv, int e) {
     uint64_t o = 0;
+    if constexpr (S5) return o;  // slot 4 is a register chunk bit (offi)
 #pragma unroll
     for (int i = 0; i < LOGNE; ++i)
       if ((e >> i) & 1) o += gv[TB + i];
@@ -688,11 +696,11 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       const uint64_t eo = goff(rg->gv_ld, e);
 #pragma unroll
       for (int i = 0; i < CPG; ++i) {
-        const chunk cf = ldc(pf + (eo + rg->offi_ld[i]));
+        const chunk cf = ldc(pf + (eo + rg->offi_ld[(S5 ? CPG * e : 0) + i]));
 #pragma unroll
         for (int v = 0; v < VEC; ++v) xf[16 * e + VEC * i + v] = cf.v[v];
         if constexpr (TWO) {
-          const chunk cb = ldc(pb + (eo + rg->offi_ld[i]));
+          const chunk cb = ldc(pb + (eo + rg->offi_ld[(S5 ? CPG * e : 0) + i]));
 #pragma unroll
           for (int v = 0; v < VEC; ++v) xb[16 * e + VEC * i + v] = cb.v[v];
         }
@@ -712,11 +720,11 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         chunk c;
 #pragma unroll
         for (int v = 0; v < VEC; ++v) c.v[v] = xf[16 * e + VEC * i + v];
-        stc(pf + (eo + rg->offi_st[i]), c);
+        stc(pf + (eo + rg->offi_st[(S5 ? CPG * e : 0) + i]), c);
         if constexpr (TWO) {
 #pragma unroll
           for (int v = 0; v < VEC; ++v) c.v[v] = xb[16 * e + VEC * i + v];
-          stc(pb + (eo + rg->offi_st[i]), c);
+          stc(pb + (eo + rg->offi_st[(S5 ? CPG * e : 0) + i]), c);
         }
       }
     }
@@ -736,10 +744,10 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     for (int e = 0; e < NE; ++e) {
       uint32_t te = 0;
 #pragma unroll
-      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Lc->tv[TB + i] : 0u;
+      for (int i = 0; i < LOGNE; ++i) te ^= (!S5 && ((e >> i) & 1)) ? Lc->tv[TB + i] : 0u;
 #pragma unroll
       for (int j = 0; j < RQ_R; ++j) {
-        const uint32_t u = (te ^ Lc->rp[j]) * (uint32_t)sizeof(cx);
+        const uint32_t u = (te ^ Lc->rp[(S5 ? 16 * e : 0) + j]) * (uint32_t)sizeof(cx);
         *reinterpret_cast<cx*>(__builtin_assume_aligned(bufb + (tpb ^ u), 8)) = x[16 * e + j];
       }
     }
@@ -751,10 +759,10 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     for (int e = 0; e < NE; ++e) {
       uint32_t te = 0;
 #pragma unroll
-      for (int i = 0; i < LOGNE; ++i) te ^= ((e >> i) & 1) ? Ln->tv[TB + i] : 0u;
+      for (int i = 0; i < LOGNE; ++i) te ^= (!S5 && ((e >> i) & 1)) ? Ln->tv[TB + i] : 0u;
 #pragma unroll
       for (int j = 0; j < RQ_R; ++j) {
-        const uint32_t u = (te ^ Ln->rp[j]) * (uint32_t)sizeof(cx);
+        const uint32_t u = (te ^ Ln->rp[(S5 ? 16 * e : 0) + j]) * (uint32_t)sizeof(cx);
         x[16 * e + j] = *reinterpret_cast<const cx*>(__builtin_assume_aligned(bufb + (tpnb ^ u), 8));
       }
     }
@@ -786,7 +794,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         lcur = op.mat;
         continue;
       }
-      rq_stage<TWO>(kind * 16u + op.t1, xf, xb, M, gamma, acc);
+      rq_stage<TWO>(kind * 64u + op.t1, xf, xb, M, gamma, acc);
       if (gamma) ++ri;
     }
   };

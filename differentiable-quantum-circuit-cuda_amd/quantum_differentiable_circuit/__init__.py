@@ -368,11 +368,13 @@ def fusion_schedule(qubits_number, instructions, mode, fwd_sens=None, precision=
     return ops, items
 
 
-def rq_plan(tile_bits, stages, deps=None, precision=None):
+def rq_plan(tile_bits, stages, deps=None, precision=None, slots=4):
     """The register-layout plan of a register-resident pass (qdc_rq_plan, host only).
     stages = [(kind 0 one-qubit | 1 two-qubit | 2 diagonal, t1, t2)] in tile bits; deps[i] =
-    bit mask of the earlier stages stage i must follow.  Returns (load, steps, store): the
-    load / store layouts' slots and [{"relayout": bool, "stage": i, "case": c, "slots": [4]}]."""
+    bit mask of the earlier stages stage i must follow; `slots` register slots (4, or 5 for the
+    one-wave two-state f32 kernel).  Returns (load, steps, store): the load / store layouts'
+    slots and [{"relayout": bool, "stage": i, "case": c, "slots": [slots]}] (two-qubit case
+    8 * slot(t1) + slot(t2))."""
     lib = load(precision or default_precision())
     n = len(stages)
     kinds = (C.c_uint * max(n, 1))(*[int(s[0]) for s in stages])
@@ -380,14 +382,14 @@ def rq_plan(tile_bits, stages, deps=None, precision=None):
     t2 = (C.c_uint * max(n, 1))(*[int(s[2]) for s in stages])
     dp = (C.c_ulonglong * max(n, 1))(*[int(d) for d in (deps or [0] * n)])
     cap = 2 * n + 4
-    out = (C.c_uint * (7 * cap))()
-    k = int(lib.qdc_rq_plan(tile_bits, kinds, t1, t2, dp, n, out, cap))
+    out = (C.c_uint * (8 * cap))()
+    k = int(lib.qdc_rq_plan(tile_bits, slots, kinds, t1, t2, dp, n, out, cap))
     if k == 2**64 - 1:
         raise RuntimeError("rq plan output capacity exceeded")
-    rows = [[int(out[7 * i + j]) for j in range(7)] for i in range(k)]
-    steps = [{"relayout": r[0] == 1, "stage": r[1], "case": r[2], "slots": r[3:7]}
+    rows = [[int(out[8 * i + j]) for j in range(8)] for i in range(k)]
+    steps = [{"relayout": r[0] == 1, "stage": r[1], "case": r[2], "slots": r[3:3 + slots]}
              for r in rows[1:-1]]
-    return rows[0][3:7], steps, rows[-1][3:7]
+    return rows[0][3:3 + slots], steps, rows[-1][3:3 + slots]
 
 
 # ---------------------------------------------------------------------------------------

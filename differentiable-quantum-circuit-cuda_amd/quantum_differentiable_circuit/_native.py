@@ -115,7 +115,7 @@ def _proto(lib):
         "qdc_abi_sync": (_E, []),
         "qdc_abi_profile": (_E, [C.c_int]),
         "qdc_abi_profile_collect": (_S, [C.POINTER(KernelStat), _S]),
-        "qdc_rq_plan": (_S, [C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+        "qdc_rq_plan": (_S, [C.c_uint, C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                              C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong), _S,
                              C.POINTER(C.c_uint), _S]),
     }

@@ -190,12 +190,13 @@ size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t first_injec
 
 /* Test hook (host only): the register-layout plan of a register-resident pass (qdc_rq.hpp)
  * over n stages with kinds[] (0 one-qubit, 1 two-qubit, 2 diagonal) on tile bits t1[], t2[]
- * (t1 < t2; one-qubit: t1 == t2) of a tile with tile_bits amplitude bits; deps[i] = bit mask
- * of the earlier stages stage i must follow (NULL: none).  steps[7*i..]: {type (2 load layout,
- * 1 relayout, 0 stage, 3 store layout), stage index, slot case, layout slots 0..3}, the load
- * layout first and the store layout last.  Returns the number of steps, or SIZE_MAX if cap is
- * too small. */
-size_t qdc_rq_plan(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+ * (t1 < t2; one-qubit: t1 == t2) of a tile with tile_bits amplitude bits, on layouts of
+ * `slots` (4 or 5) register slots; deps[i] = bit mask of the earlier stages stage i must
+ * follow (NULL: none).  steps[8*i..]: {type (2 load layout, 1 relayout, 0 stage, 3 store
+ * layout), stage index, slot case (two-qubit: 8 * slot(t1) + slot(t2); one-qubit: slot),
+ * layout slots 0..4 (~0 past `slots`)}, the load layout first and the store layout last.
+ * Returns the number of steps, or SIZE_MAX if cap is too small or the arguments are invalid. */
+size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds, const unsigned* t1,
                    const unsigned* t2, const unsigned long long* deps, size_t n,
                    unsigned* steps, size_t cap);
 

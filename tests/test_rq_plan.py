@@ -7,7 +7,7 @@ A plan is valid when, replayed step by step:
     layout holds 4 distinct tile bits;
   * every stage runs exactly once, after the stages it depends on;
   * a stage runs on the current layout with its qubits in the slots its slot case names
-    (one-qubit: the slot of t1; two-qubit / diagonal: 4 * slot(t1) + slot(t2)).
+    (one-qubit: the slot of t1; two-qubit / diagonal: 8 * slot(t1) + slot(t2)).
 The max-closure planner (default) must not need more relayouts in total than the greedy one
 (QDC_RQ_MAXCL=0) on brickwork-like and random passes.
 """
@@ -35,7 +35,7 @@ def random_pass(rng, T, nst, brick=False):
     return stages, deps
 
 
-def check_plan(T, stages, deps, plan, prec="f32"):
+def check_plan(T, stages, deps, plan, prec="f32", slots=4):
     load, steps, store = plan
 
     def hbm_ok(L):
@@ -47,7 +47,7 @@ def check_plan(T, stages, deps, plan, prec="f32"):
     cur, done, relayouts = list(load), set(), 0
     for s in steps:
         L = s["slots"]
-        assert len(set(L)) == 4 and all(q < T for q in L), L
+        assert len(set(L)) == slots and all(q < T for q in L), L
         if s["relayout"]:
             cur, relayouts = list(L), relayouts + 1
             continue
@@ -58,16 +58,17 @@ def check_plan(T, stages, deps, plan, prec="f32"):
         if kind == Q1:
             assert cur[s["case"]] == t1
         else:
-            assert cur[s["case"] // 4] == t1 and cur[s["case"] % 4] == t2
+            assert cur[s["case"] // 8] == t1 and cur[s["case"] % 8] == t2
         done.add(j)
     assert done == set(range(len(stages)))
     assert cur == list(store)
     return relayouts
 
 
-@pytest.mark.parametrize("prec,T", [("f32", 11), ("f32", 12), ("f64", 10), ("f64", 11)])
+@pytest.mark.parametrize("prec,T,slots", [("f32", 11, 4), ("f32", 12, 4), ("f32", 11, 5),
+                                           ("f64", 10, 4), ("f64", 11, 4)])
 @pytest.mark.parametrize("brick", [False, True])
-def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, prec, T, brick):
+def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, prec, T, slots, brick):
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(T * 2 + brick)
     total = {"1": 0, "0": 0}
@@ -75,6 +76,24 @@ def test_rq_plan_valid_and_max_closure_not_worse(monkeypatch, prec, T, brick):
         stages, deps = random_pass(rng, T, int(rng.integers(1, 40)), brick)
         for mc in ("1", "0"):
             monkeypatch.setenv("QDC_RQ_MAXCL", mc)
-            total[mc] += check_plan(T, stages, deps, q.rq_plan(T, stages, deps, precision=prec),
-                                    prec)
+            total[mc] += check_plan(T, stages, deps,
+                                    q.rq_plan(T, stages, deps, precision=prec, slots=slots),
+                                    prec, slots)
     assert total["1"] <= total["0"], total
+
+
+@pytest.mark.parametrize("brick", [False, True])
+def test_rq_plan_five_slots_fewer_relayouts(brick):
+    """A fifth register slot (the one-wave two-state kernel's register-group bit) holds covers
+    of 5 qubits: never more relayouts than 4 slots over a set of passes."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(7 + brick)
+    total = {4: 0, 5: 0}
+    for _ in range(120):
+        stages, deps = random_pass(rng, 11, int(rng.integers(4, 40)), brick)
+        for sl in (4, 5):
+            total[sl] += check_plan(11, stages, deps,
+                                    q.rq_plan(11, stages, deps, precision="f32", slots=sl),
+                                    "f32", sl)
+    print("relayouts 4 / 5 slots:", total)
+    assert total[5] < total[4], total
