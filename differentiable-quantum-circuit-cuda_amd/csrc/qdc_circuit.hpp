@@ -839,7 +839,9 @@ struct Circuit {
         }
       }
       // five register slots on the one-wave two-state f32 kernel (k_rw<.., S5>)
-      const uint32_t ns = (sizeof(real) == 4 && two && rq5()) ? 5u : 4u;
+      const bool s5_two = two && rq5();
+      const bool s5_one = !two && rq_slots5 && (rq_wave & 2) && it.tbits == 11;  // k_rw W = 1
+      const uint32_t ns = (sizeof(real) == 4 && (s5_two || s5_one)) ? 5u : 4u;
       it.s5 = ns == 5;
       const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
       it.l0 = put_layout(P.load);
@@ -939,11 +941,14 @@ struct Circuit {
       // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);
       const uint32_t bs = (!two && nt == 256) ? 128u : 64u;
-      if (s5 && !(two && !pfw)) return fail("internal: a five-slot pass without its kernel");
+      if (s5 && !((two && !pfw) || (!two && nt == 128)))
+        return fail("internal: a five-slot pass without its kernel");
       const void* kw = two ? (pfw  ? (const void*)k_rw<true, 2, true, 1>
                               : s5 ? (const void*)k_rw<true, 2, false, 1, true>
                                    : (const void*)k_rw<true, 2, false, 1>)
-                           : nt == 128 ? (const void*)k_rw<false, 2, false, 1> : (const void*)k_rw<false, 2, false, 2>;
+                           : nt == 128 ? (s5 ? (const void*)k_rw<false, 2, false, 1, true>
+                                             : (const void*)k_rw<false, 2, false, 1>)
+                                       : (const void*)k_rw<false, 2, false, 2>;
       uint32_t grid = 0;
       QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
       fgeo g = fg;
@@ -962,6 +967,9 @@ struct Circuit {
       if (two)
         return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
+      if (nt == 128 && s5)
+        return ctx.launch_block(name, bytes, k_rw<false, 2, false, 1, true>, grid, bs, f, b, fops,
+                                mats, g, l0, partials, stride);
       if (nt == 128)
         return ctx.launch_block(name, bytes, k_rw<false, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
