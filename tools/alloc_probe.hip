@@ -86,6 +86,80 @@ __global__ __launch_bounds__(256) void k_pair1(vec4* __restrict__ f, uint32_t lb
   st(f + c1, x1 * 1.0000001f);
 }
 
+// one-state quad: chunks c0 + {0, 2^lb, 2^lb2, 2^lb + 2^lb2}, lb2 < lb (a far pair split over a
+// second, near "bank" bit)
+__global__ __launch_bounds__(256) void k_quad1(vec4* __restrict__ f, uint32_t lb, uint32_t lb2) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t lo = j & ((1ull << lb2) - 1);
+  uint64_t c0 = ((j - lo) << 1) | lo;
+  lo = c0 & ((1ull << lb) - 1);
+  c0 = ((c0 - lo) << 1) | lo;
+  const uint64_t o[4] = {0, 1ull << lb2, 1ull << lb, (1ull << lb) + (1ull << lb2)};
+  vec4 x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = ld(f + c0 + o[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st(f + c0 + o[k], x[k] * 1.0000001f);
+}
+
+// one-state pair with the block order swizzled: block b runs item block b ^ (b >> s & m)
+__global__ __launch_bounds__(256) void k_pair1s(vec4* __restrict__ f, uint32_t lb, uint32_t sh, uint32_t m) {
+  const uint64_t bb = blockIdx.x ^ ((blockIdx.x >> sh) & m);
+  const uint64_t j = bb * 256 + threadIdx.x;
+  const uint64_t lo = j & ((1ull << lb) - 1);
+  const uint64_t c0 = ((j - lo) << 1) | lo, c1 = c0 + (1ull << lb);
+  vec4 x0 = ld(f + c0), x1 = ld(f + c1);
+  st(f + c0, x0 * 1.0000001f);
+  st(f + c1, x1 * 1.0000001f);
+}
+
+// two-state, block-contiguous: block b owns items [b*256*it, (b+1)*256*it), U in flight
+template <int U>
+__global__ __launch_bounds__(256) void k_blk2(vec4* __restrict__ f, vec4* __restrict__ b, uint32_t it) {
+  const uint64_t start = (uint64_t)blockIdx.x * 256 * it + threadIdx.x;
+  for (uint32_t s = 0; s < it; s += U) {
+    vec4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = ld(f + start + (uint64_t)(s + u) * 256);
+      y[u] = ld(b + start + (uint64_t)(s + u) * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st(f + start + (uint64_t)(s + u) * 256, x[u] * 1.0000001f);
+      st(b + start + (uint64_t)(s + u) * 256, y[u] * 0.9999999f);
+    }
+  }
+}
+// two-state, grid-strided over 256-item blocks: round s of block b runs item block s*grid + b
+// (the resident blocks sweep one contiguous window together)
+template <int U>
+__global__ __launch_bounds__(256) void k_win2(vec4* __restrict__ f, vec4* __restrict__ b, uint32_t it) {
+  for (uint32_t s = 0; s < it; s += U) {
+    vec4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = ((uint64_t)(s + u) * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+      x[u] = ld(f + i);
+      y[u] = ld(b + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = ((uint64_t)(s + u) * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+      st(f + i, x[u] * 1.0000001f);
+      st(b + i, y[u] * 0.9999999f);
+    }
+  }
+}
+
+// one state of an interleaved pair (every other 2^g-chunk block of the buffer)
+__global__ __launch_bounds__(256) void k_ilv1(vec4* __restrict__ buf, uint32_t g) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t lo = j & ((1ull << g) - 1);
+  const uint64_t c = ((j - lo) << 1) | lo;
+  st(buf + c, ld(buf + c) * 1.0000001f);
+}
+
 template <int NS>
 __global__ __launch_bounds__(256) void k_rmw(vec4* __restrict__ f, vec4* __restrict__ b) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -125,52 +199,37 @@ int main() {
   };
   auto tb1 = [&](vec4* f) { return 2.0 * S / timeit([&] { k_rmw<1><<<grid, 256>>>(f, f); }) / 1e9; };
   for (int trial = 0; trial < 4; ++trial) {
-    vec4 *ini, *st_, *bwd;
-    CK(hipMalloc(&ini, S));
-    CK(hipMalloc(&st_, S));
-    CK(hipMemset(ini, 0, S));
-    CK(hipMemset(st_, 0, S));
-    CK(hipMalloc(&bwd, S));
-    CK(hipMemset(bwd, 0, S));
-    const long long d1 = (long long)((char*)bwd - (char*)st_);
-    printf("trial %d pair strides (chunk bit: TB/s):", trial);
-    for (uint32_t lb : {6u, 9u, 10u, 11u, 12u, 13u, 14u, 16u, 20u})
-      printf(" %u:%.2f", lb,
-             4.0 * S / timeit([&] { k_pair<<<grid / 2, 256>>>(st_, bwd, lb); }) / 1e9);
-    printf("\n");
-    printf("trial %d quad lb=6, lb2:", trial);
-    for (uint32_t lb2 : {9u, 10u, 11u, 12u, 13u, 14u, 16u})
-      printf(" %u:%.2f", lb2,
-             4.0 * S / timeit([&] { k_quad<<<grid / 4, 256>>>(st_, bwd, 6, lb2); }) / 1e9);
-    printf("\n");
-    printf("trial %d quad lb=16, lb2:", trial);
-    for (uint32_t lb2 : {17u, 18u, 20u, 24u})
-      printf(" %u:%.2f", lb2,
-             4.0 * S / timeit([&] { k_quad<<<grid / 4, 256>>>(st_, bwd, 16, lb2); }) / 1e9);
-    printf("\n");
-    printf("trial %d ini %p st %p bwd %p (bwd-st %+lld MiB)  1st: st %.2f bwd %.2f  "
-           "2st: st/bwd %.2f ini/st %.2f ini/bwd %.2f TB/s\n",
-           trial, (void*)ini, (void*)st_, (void*)bwd, d1 >> 20, tb1(st_), tb1(bwd), tb2(st_, bwd),
-           tb2(ini, st_), tb2(ini, bwd));
-    fflush(stdout);
-    CK(hipFree(bwd));
-    CK(hipFree(st_));
-    CK(hipFree(ini));
-  }
-  for (int trial = 0; trial < 4; ++trial) {
-    vec4* buf;
-    CK(hipMalloc(&buf, 2 * S));
-    CK(hipMemset(buf, 0, 2 * S));
-    printf("trial %d interleaved 2-state (g: TB/s):", trial);
-    for (uint32_t g : {6u, 8u, 10u, 12u, 14u, 16u, 17u, 20u})
-      printf(" %u:%.2f", g, 4.0 * S / timeit([&] { k_ilv<<<grid, 256>>>(buf, g); }) / 1e9);
-    printf("  split halves: %.2f\n", tb2(buf, buf + nch));
-    printf("trial %d one-state pairs in the first half (chunk bit: TB/s):", trial);
-    for (uint32_t lb = 0; lb < 27; ++lb)
-      printf(" %u:%.2f", lb, 2.0 * S / timeit([&] { k_pair1<<<grid / 2, 256>>>(buf, lb); }) / 1e9);
+    vec4 *fa, *ba;
+    CK(hipMalloc(&fa, S));
+    CK(hipMalloc(&ba, S));
+    CK(hipMemset(fa, 0, S));
+    CK(hipMemset(ba, 0, S));
+    printf("trial %d 2-state blk (it:TB/s):", trial);
+    for (uint32_t it : {1u, 2u, 4u, 8u, 16u, 64u, 256u})
+      printf(" %u:%.2f", it, 4.0 * S / timeit([&] { k_blk2<1><<<grid / it, 256>>>(fa, ba, it); }) / 1e9);
+    printf("  U2:");
+    for (uint32_t it : {2u, 8u, 64u, 256u})
+      printf(" %u:%.2f", it, 4.0 * S / timeit([&] { k_blk2<2><<<grid / it, 256>>>(fa, ba, it); }) / 1e9);
+    printf("  win (it):");
+    for (uint32_t it : {4u, 16u, 64u, 256u})
+      printf(" %u:%.2f", it, 4.0 * S / timeit([&] { k_win2<1><<<grid / it, 256>>>(fa, ba, it); }) / 1e9);
+    printf("  ilv1 (g):");
+    {
+      vec4* buf;
+      CK(hipMalloc(&buf, 2 * S));
+      CK(hipMemset(buf, 0, 2 * S));
+      for (uint32_t g : {10u, 12u, 14u})
+        printf(" %u:%.2f/%.2f", g, 2.0 * S / timeit([&] { k_ilv1<<<grid, 256>>>(buf, g); }) / 1e9,
+               4.0 * S / timeit([&] { k_ilv<<<grid, 256>>>(buf, g); }) / 1e9);
+      CK(hipFree(buf));
+    }
+    printf("  winU2:");
+    for (uint32_t it : {64u, 256u})
+      printf(" %u:%.2f", it, 4.0 * S / timeit([&] { k_win2<2><<<grid / it, 256>>>(fa, ba, it); }) / 1e9);
     printf("\n");
     fflush(stdout);
-    CK(hipFree(buf));
+    CK(hipFree(fa));
+    CK(hipFree(ba));
   }
   return 0;
 }
