@@ -86,8 +86,7 @@ QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
   if (!src) return qdc::fail("state %d is not allocated", which);
   QDC_TRY(k.sync_all());  // every shard's work, not only this shard's stream
   QDC_TRY(s.c().use());
-  QDC_HIP(hipMemcpyAsync(host, src, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
-                         s.c().stream));
+  QDC_TRY(k.read_state(s, src, 0, host, len));
   QDC_HIP(hipStreamSynchronize(s.c().stream));
   return nullptr;
 }
@@ -105,8 +104,7 @@ QDC_API const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, 
   if (!src) return qdc::fail("state %d is not allocated", which);
   QDC_TRY(k.sync_all());
   QDC_TRY(s.c().use());
-  QDC_HIP(hipMemcpyAsync(host, src + offset, len * sizeof(qdc_complex), hipMemcpyDeviceToHost,
-                         s.c().stream));
+  QDC_TRY(k.read_state(s, src, offset, host, len));
   QDC_HIP(hipStreamSynchronize(s.c().stream));
   return nullptr;
 }

@@ -86,6 +86,7 @@ struct Shard {
   cx* state = nullptr;
   cx* bwd = nullptr;
   cx* scratch = nullptr;  // all-to-all staging (allocated when world > 1)
+  std::vector<void*> owned;  // state allocations (remaps swap the pointers above among them)
   cx* dens = nullptr;
   cx* grads = nullptr;
   DevRes* d = nullptr;  // the shard's device resources
@@ -207,6 +208,10 @@ struct Circuit {
   uint32_t n = 0;   // logical qubits
   uint32_t g = 0;   // rank bits
   uint32_t nl = 0;  // local qubits of a shard
+  // interleaved state pair (unsharded): fwd and bwd alternate in 2^gap_bits-chunk blocks of one
+  // allocation; chunk c of either state at c + (c & gm), bwd = fwd + 2^gap_bits chunks
+  uint32_t gap_bits = 0;
+  uint64_t gm = 0;
   std::vector<std::unique_ptr<DevRes>> devs;  // per-device resources (sh[s].d points here)
   Exchange ex;
   std::vector<Shard> sh;
@@ -312,14 +317,18 @@ struct Circuit {
       Ctx& c = sh[s].c();
       QDC_TRY(c.use());
       QDC_HIP(hipMalloc(&sh[s].initial, bytes));
-      QDC_HIP(hipMalloc(&sh[s].state, bytes));
-      if (g > 0) QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
+      sh[s].owned.push_back(sh[s].initial);
+      QDC_TRY(alloc_pair(sh[s], bytes));
+      if (g > 0) {
+        QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
+        sh[s].owned.push_back(sh[s].scratch);
+      }
       // QuantizedTensor::new_standard + clone (circuit.rs:96-102): |0..0> lives on shard 0
       if (rank0 + s == 0)
         QDC_TRY(set_standard(c, sh[s].initial, nl));
       else
         QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, c.stream));
-      QDC_TRY(elementwise<0>(c, sh[s].initial, sh[s].state, nl));
+      QDC_TRY(copy_initial(sh[s]));
     }
     QDC_TRY(sync_all());
     QDC_HIP(hipSetDevice(cur));
@@ -329,7 +338,8 @@ struct Circuit {
     (void)sync_all();
     for (auto& s : sh) {
       if (s.d) (void)s.d->ctx.use();
-      for (cx* p : {s.initial, s.state, s.bwd, s.scratch, s.dens, s.grads})
+      for (void* p : s.owned) (void)hipFree(p);
+      for (cx* p : {s.dens, s.grads})
         if (p) (void)hipFree(p);
     }
     sh.clear();
@@ -345,6 +355,81 @@ struct Circuit {
     if (prog_host) (void)hipHostFree(prog_host);
     prog_host = nullptr;
     ex.destroy();
+  }
+
+  // The forward and cotangent states as one allocation, interleaved in 64 KiB blocks (chunk
+  // bit 12 selects the state).  Two states streamed together then run at one steady rate
+  // whatever the placement (6.5 TB/s for in-place fwd+bwd at n = 28), while two separate 2 GiB
+  // allocations land on placements that stream at 5.0-6.5 TB/s and the single-gate reverse
+  // kernels at 64 % or 79 % of 8 TB/s from one circuit to the next (tools/alloc_probe.hip,
+  // tools/pair_probe.hip, profiles/r2e_*, r2f_*).  Unsharded circuits only (a remap swaps the
+  // states with the scratch buffer); QDC_STATE_ILV=0 keeps the plain layout (bwd separate and
+  // allocated on the first backward).
+  const char* alloc_pair(Shard& s, size_t bytes) {
+    const char* e = getenv("QDC_STATE_ILV");
+    // states of at least two blocks (smaller ones gain nothing)
+    const bool ilv = !(e && atoi(e) == 0) && g == 0 && sh.size() == 1 && nchunks_of(nl) >= 8192;
+    if (ilv) {
+      gap_bits = 12;
+      gm = ~(((uint64_t)1 << gap_bits) - 1);
+      char* blk = nullptr;
+      QDC_HIP(hipMalloc(&blk, 2 * bytes));
+      s.owned.push_back(blk);
+      s.state = (cx*)blk;
+      s.bwd = (cx*)blk + ((size_t)VEC << gap_bits);
+      s.c().gm = gm;
+    } else {
+      QDC_HIP(hipMalloc(&s.state, bytes));
+      s.owned.push_back(s.state);
+    }
+    return nullptr;
+  }
+  // geometry of one state of an interleaved pair as a 2-D copy: rows of 2^gap_bits chunks at a
+  // pitch of two rows
+  size_t ilv_width() const { return ((size_t)sizeof(cx) * VEC) << gap_bits; }
+  size_t ilv_rows() const { return nchunks_of(nl) >> gap_bits; }
+  const char* copy_initial(Shard& s) {
+    if (!gm) return elementwise<0>(s.c(), s.initial, s.state, nl);
+    QDC_HIP(hipMemcpy2DAsync(s.state, 2 * ilv_width(), s.initial, ilv_width(), ilv_width(),
+                             ilv_rows(), hipMemcpyDeviceToDevice, s.c().stream));
+    return nullptr;
+  }
+  const char* zero_bwd(Shard& s) {
+    if (!gm) {
+      QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));
+    } else {
+      QDC_HIP(hipMemset2DAsync(s.bwd, 2 * ilv_width(), 0, ilv_width(), ilv_rows(), s.c().stream));
+    }
+    return nullptr;
+  }
+  // host copy of amplitudes [offset, offset + len) of a (possibly interleaved) state
+  const char* read_state(const Shard& s, const cx* src, size_t offset, qdc_complex* host,
+                         size_t len) {
+    const hipStream_t st = s.c().stream;
+    if (!gm || (src != s.state && src != s.bwd)) {
+      QDC_HIP(hipMemcpyAsync(host, src + offset, len * sizeof(cx), hipMemcpyDeviceToHost, st));
+      return nullptr;
+    }
+    const size_t row = (size_t)VEC << gap_bits;  // amplitudes per block
+    size_t o = offset, done = 0;
+    auto piece = [&](size_t cnt) -> const char* {  // within one block
+      const size_t phys = (o / row) * 2 * row + o % row;
+      QDC_HIP(hipMemcpyAsync(host + done, src + phys, cnt * sizeof(cx), hipMemcpyDeviceToHost, st));
+      o += cnt;
+      done += cnt;
+      return nullptr;
+    };
+    if (o % row && done < len) QDC_TRY(piece(std::min(len - done, row - o % row)));
+    const size_t full = (len - done) / row;
+    if (full) {
+      QDC_HIP(hipMemcpy2DAsync(host + done, row * sizeof(cx), src + (o / row) * 2 * row,
+                               2 * row * sizeof(cx), row * sizeof(cx), full,
+                               hipMemcpyDeviceToHost, st));
+      o += full * row;
+      done += full * row;
+    }
+    if (done < len) QDC_TRY(piece(len - done));
+    return nullptr;
   }
 
   const char* ensure_out(bool dens, size_t count) {
@@ -849,6 +934,12 @@ struct Circuit {
         rqio io{};
         rq_hbm(P.load, it.tbits, it.lc, it.hb, io.gv_ld, io.offi_ld);
         rq_hbm(P.store, it.tbits, it.lc, it.hb, io.gv_st, io.offi_st, perm ? dest : nullptr);
+        // gapped offsets (interleaved pair): the kernel gaps only the tile base, and the gap
+        // is linear over the disjoint bit sets of base, thread and register offsets
+        for (uint64_t* a : {io.gv_ld, io.gv_st})
+          for (int k = 0; k < 8; ++k) a[k] += a[k] & gm;
+        for (uint64_t* a : {io.offi_ld, io.offi_st})
+          for (int k = 0; k < RQ_R; ++k) a[k] += a[k] & gm;
         std::memcpy(&mats[mo], &io, sizeof io);
         mo += sizeof(rqio) / sizeof(cx);
       }
@@ -1062,6 +1153,7 @@ struct Circuit {
   const char* run_fused(const Item& it, bool two, size_t mats_off, bool red_to_grads) {
     fgeo fg{};
     fg.order = it.rq ? (uint32_t)rq_order : 0u;
+    fg.gm = gm;
     fg.lc = it.lc;
     fg.h = it.h;
     for (uint32_t k = 0; k < FMAX_ROWS; ++k) fg.hb[k] = it.hb[k];
@@ -1156,7 +1248,7 @@ struct Circuit {
     layout.identity(n, g);
     for (auto& s : sh) {
       QDC_TRY(s.c().use());
-      QDC_TRY(elementwise<0>(s.c(), s.initial, s.state, nl));
+      QDC_TRY(copy_initial(s));
     }
     std::vector<uint32_t> out_idx(ins.size(), 0);
     {
@@ -1242,6 +1334,7 @@ struct Circuit {
       if (!s.bwd) {
         QDC_TRY(s.c().use());
         QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
+        s.owned.push_back(s.bwd);
       }
     // slots [0, nvar): per-gate gradients; [nvar, nvar + stages): fused stages' Gamma
     const size_t nslots = std::max<size_t>(2 * nvar, 1);
@@ -1280,7 +1373,7 @@ struct Circuit {
         if (two && !have_bwd) {  // the first injection is fused: it adds into a zero bwd
           for (auto& s : sh) {
             QDC_TRY(s.c().use());
-            QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));
+            QDC_TRY(zero_bwd(s));
           }
           have_bwd = true;
         }

@@ -98,6 +98,10 @@ struct Ctx {
   uint32_t grid_cap = 1u << 20;  // streaming launches: ~one item per thread (measured best)
   uint32_t red_cap = 2048;   // target blocks of reduction launches (<= NBMAX)
   double next_flops = 0;     // algorithmic FLOPs of the next launch (profiling; reset by launch)
+  // gap mask of the states this context's gate-shaped launches address: chunk c of a state at
+  // c + (c & gm).  Nonzero for a circuit whose fwd / bwd states are interleaved in one
+  // allocation (qdc_circuit.hpp alloc_pair); 0 (plain) for the primitives' states.
+  uint64_t gm = 0;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -429,7 +433,10 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
 template <int R>
 inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
                      bool reduces) {
-  return plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap);
+  Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap);
+  p.g.gm = c.gm;
+  p.tg.gm = c.gm;
+  return p;
 }
 
 template <int R>
@@ -439,8 +446,9 @@ inline const char* apply_dense(Ctx& c, cx* s, const mat<R>& m, uint32_t pos2, ui
   return run_op<OP_APPLY, R>(c, name, 2.0 * state_bytes(n), s, nullptr, m, m, p, nullptr);
 }
 
-inline dgeo diag_geo(uint32_t n, uint32_t pos2, uint32_t pos1, uint32_t target) {
+inline dgeo diag_geo(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, uint32_t target) {
   dgeo g;
+  g.gm = c.gm;
   g.nchunks = nchunks_of(n);
   g.it = per_thread(g.nchunks, target);
   g.p2 = pos2;
@@ -453,7 +461,7 @@ inline uint32_t diag_blocks(const dgeo& g) {
 
 inline const char* apply_diag(Ctx& c, cx* s, const diag4& d, uint32_t pos2, uint32_t pos1,
                               uint32_t n, const char* name) {
-  const dgeo g = diag_geo(n, pos2, pos1, c.grid_cap);
+  const dgeo g = diag_geo(c, n, pos2, pos1, c.grid_cap);
   return c.launch(name, 2.0 * state_bytes(n), k_diag<DIAG_APPLY, 4>, diag_blocks(g),
                   reinterpret_cast<chunk*>(s), (chunk*)nullptr, d, d, g, (cx*)nullptr);
 }
@@ -494,7 +502,7 @@ inline const char* grad_dense(Ctx& c, const cx* f, const cx* b, uint32_t pos2, u
 
 inline const char* grad_diag(Ctx& c, const cx* f, const cx* b, uint32_t pos2, uint32_t pos1,
                              uint32_t n, cx* base, uint32_t dst, int accumulate) {
-  const dgeo g = diag_geo(n, pos2, pos1, c.red_cap);
+  const dgeo g = diag_geo(c, n, pos2, pos1, c.red_cap);
   const diag4 z{};
   return reduce_into(c, base, dst, accumulate, diag_blocks(g), [&](cx* out) {
     return c.launch("grad_q2_diag", 2.0 * state_bytes(n), k_diag<DIAG_GRAD, 4>, diag_blocks(g),
@@ -527,13 +535,13 @@ inline const char* reverse_diag(Ctx& c, cx* f, cx* b, const diag4& d, uint32_t p
   const diag4 dc = conj_diag(d);
   const double bytes = 4.0 * state_bytes(n);
   if (grad_base) {
-    const dgeo g = diag_geo(n, pos2, pos1, c.red_cap);
+    const dgeo g = diag_geo(c, n, pos2, pos1, c.red_cap);
     return reduce_into(c, grad_base, dst, 0, diag_blocks(g), [&](cx* out) {
       return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE_GRAD, 2>, diag_blocks(g), fc,
                       bc, dc, d, g, out);
     });
   }
-  const dgeo g = diag_geo(n, pos2, pos1, c.grid_cap);
+  const dgeo g = diag_geo(c, n, pos2, pos1, c.grid_cap);
   return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE, 2>, diag_blocks(g), fc, bc, dc,
                   d, g, (cx*)nullptr);
 }

@@ -208,6 +208,7 @@ struct geo {
   uint32_t lo;     // chunk bit positions for zero insertion (lower first)
   uint32_t hi;
   uint32_t it;     // items per thread (block-contiguous iteration)
+  uint64_t gm;     // gap mask: chunk c of a state lives at c + (c & gm) (interleaved pair)
 };
 
 template <int R, int MODE>
@@ -297,6 +298,8 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
       const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
       ok[u] = (step + u < g.it) && i < g.items;
       L::chunks(g, ok[u] ? i : 0, c[u]);
+#pragma unroll
+      for (int k = 0; k < L::NC; ++k) c[u][k] += c[u][k] & g.gm;
       if (ok[u]) {
 #pragma unroll
         for (int k = 0; k < L::NC; ++k) {
@@ -342,6 +345,7 @@ struct tgeo {
   uint32_t h;      // row bits (0..2)
   uint32_t hb0, hb1;  // global chunk bit of row bit 0 / 1
   uint32_t t1, t2;    // tile-local amplitude bits of the gate's index bits 0 (pos1) and 1 (pos2)
+  uint64_t gm;        // gap mask (geo::gm)
 };
 
 __device__ __forceinline__ uint64_t tile_base(const tgeo& tg, uint64_t tile) {
@@ -384,6 +388,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
     for (int k = 0; k < K; ++k) {
       if (k * BLOCK + t >= tc) break;
       gi[k] = tile_chunk(tg, base, k * BLOCK + t);
+      gi[k] += gi[k] & tg.gm;
       rf[k] = ldc(f + gi[k]);
       if constexpr (op_reads_b(OP)) rb[k] = ldc(b + gi[k]);
     }
@@ -455,6 +460,7 @@ struct dgeo {
   uint64_t nchunks;
   uint32_t it;
   uint32_t p2, p1;
+  uint64_t gm;  // gap mask (geo::gm)
 };
 
 template <int OP, int U>
@@ -473,8 +479,8 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
       const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
       ok[u] = (step + u < g.it) && i < g.nchunks;
       if (ok[u]) {
-        fc[u] = ldc(f + i);
-        if constexpr (TWO) bc[u] = ldc(b + i);
+        fc[u] = ldc(f + (i + (i & g.gm)));
+        if constexpr (TWO) bc[u] = ldc(b + (i + (i & g.gm)));
       }
     }
 #pragma unroll
@@ -503,8 +509,8 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
           bc[u].v[v] = cmul(pick4(d, k), bc[u].v[v]);
         }
       }
-      if constexpr (OP != DIAG_GRAD) stc(f + i, fc[u]);
-      if constexpr (OP == DIAG_REVERSE || OP == DIAG_REVERSE_GRAD) stc(b + i, bc[u]);
+      if constexpr (OP != DIAG_GRAD) stc(f + (i + (i & g.gm)), fc[u]);
+      if constexpr (OP == DIAG_REVERSE || OP == DIAG_REVERSE_GRAD) stc(b + (i + (i & g.gm)), bc[u]);
     }
   }
   if constexpr (RED_) block_reduce_store<4>(acc, partials + (uint64_t)blockIdx.x * RED);
@@ -583,6 +589,8 @@ struct fgeo {
   uint32_t nops;
   uint32_t ngrad;  // reduction ops (Gamma stages, densities): partials in consecutive slots
   uint32_t order;  // register-resident passes: 0 block-contiguous tiles, 1 grid-strided
+  uint64_t gm;     // gap mask (geo::gm); register-resident passes get their rqio offsets gapped
+                   // on the host, so only the tile base is gapped here
 };
 
 // Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the
@@ -870,14 +878,14 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) o += (uint64_t)((c >> (fg.lc + k)) & 1u) << fg.hb[k];
-    off[i] = o;
+    off[i] = o + (o & fg.gm);
   }
   auto tile_base = [&](uint64_t tile) {
     uint64_t base = tile << fg.lc;
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    return base;
+    return base + (base & fg.gm);
   };
   // software pipeline: the next tile's chunks are in flight while this tile's ops run
   chunk pf[NS][CPT];

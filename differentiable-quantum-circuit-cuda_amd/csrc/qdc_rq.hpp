@@ -455,7 +455,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    return base;
+    return base + (base & fg.gm);
   };
   // re-read per use, so the compiler does not hold the offsets in SGPRs across the pass
   auto rqio_now = [&]() {
@@ -671,7 +671,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
       if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    return base;
+    return base + (base & fg.gm);
   };
   auto rqio_now = [&]() {
     uint32_t ro = l0;
