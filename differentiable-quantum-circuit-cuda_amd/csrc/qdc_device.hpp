@@ -102,6 +102,10 @@ struct Ctx {
   // c + (c & gm).  Nonzero for a circuit whose fwd / bwd states are interleaved in one
   // allocation (qdc_circuit.hpp alloc_pair); 0 (plain) for the primitives' states.
   uint64_t gm = 0;
+  // minimum items per thread of streaming (non-reducing) direct / diagonal launches (knob
+  // QDC_DIRECT_IT; 0: one item per thread).  tools/pair_probe.hip streams a far q1 pair at
+  // 5.3 / 5.55 / 5.9 TB/s with 1 / 2 / 4 items per thread in flight
+  uint32_t direct_it = 0;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -121,6 +125,7 @@ struct Ctx {
     QDC_HIP(hipHostMalloc(&host_results, sizeof(cx) * (size_t)FIN_MAX * RED));
     if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
@@ -403,6 +408,10 @@ inline const char* inverse(const mat<R>& a, mat<R>& out) {
 // ---------------------------------------------------------------------------------------
 inline double state_bytes(uint32_t n) { return (double)((uint64_t)1 << n) * sizeof(cx); }
 
+// items in flight per thread and step of the direct family: 4 q1 items (8 chunks per state),
+// 2 q2 items
+constexpr int direct_u(int R) { return R == 2 ? 4 : 2; }
+
 inline uint32_t blocks_of(const Plan& p) {
   if (p.tile) return (uint32_t)((p.tg.ntiles + p.tg.tpb - 1) / p.tg.tpb);
   return (uint32_t)((p.g.items + (uint64_t)BLOCK * p.g.it - 1) / ((uint64_t)BLOCK * p.g.it));
@@ -420,13 +429,13 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
     return c.launch(name, bytes, k_tile<OP, R, K>, grid, fc, bc, A, B, p.tg, partials);
   }
   if (p.mode == 0)
-    return c.launch(name, bytes, k_direct<OP, R, 0, (R == 2 ? 2 : 1)>, grid, fc, bc, A, B, p.g,
+    return c.launch(name, bytes, k_direct<OP, R, 0, direct_u(R)>, grid, fc, bc, A, B, p.g,
                     partials);
   if (p.mode == 1)
-    return c.launch(name, bytes, k_direct<OP, R, 1, (R == 2 ? 4 : 2)>, grid, fc, bc, A, B, p.g,
+    return c.launch(name, bytes, k_direct<OP, R, 1, direct_u(R)>, grid, fc, bc, A, B, p.g,
                     partials);
   if constexpr (R == 4)
-    return c.launch(name, bytes, k_direct<OP, 4, 2, 2>, grid, fc, bc, A, B, p.g, partials);
+    return c.launch(name, bytes, k_direct<OP, 4, 2, direct_u(4)>, grid, fc, bc, A, B, p.g, partials);
   return fail("invalid plan");
 }
 
@@ -434,6 +443,7 @@ template <int R>
 inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
                      bool reduces) {
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap);
+  if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
   return p;
@@ -451,6 +461,7 @@ inline dgeo diag_geo(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, uin
   g.gm = c.gm;
   g.nchunks = nchunks_of(n);
   g.it = per_thread(g.nchunks, target);
+  if (target == c.grid_cap && g.it < c.direct_it) g.it = c.direct_it;  // streaming
   g.p2 = pos2;
   g.p1 = pos1;
   return g;

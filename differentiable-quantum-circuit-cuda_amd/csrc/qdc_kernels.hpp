@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace qdc {
 
 #ifdef QDC_F64
@@ -289,6 +291,9 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
 #pragma unroll
   for (int k = 0; k < NACC; ++k) acc[k] = {0, 0};
   const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  // blocks whose items all exist (every block of a power-of-two state) run without per-item
+  // guards: a guarded load is a branch the waitcnt pass drains in-flight loads around
+  auto body = [&](auto guarded) __attribute__((always_inline)) {
   for (uint32_t step = 0; step < g.it; step += U) {
     uint64_t c[U][L::NC];
     chunk fc[U][L::NC], bc[U][L::NC];
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
-      ok[u] = (step + u < g.it) && i < g.items;
+      ok[u] = !decltype(guarded)::value || ((step + u < g.it) && i < g.items);
       L::chunks(g, ok[u] ? i : 0, c[u]);
 #pragma unroll
       for (int k = 0; k < L::NC; ++k) c[u][k] += c[u][k] & g.gm;
@@ -328,6 +333,11 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
       }
     }
   }
+  };
+  if ((uint64_t)(blockIdx.x + 1) * BLOCK * g.it <= g.items && g.it % U == 0)
+    body(std::false_type{});
+  else
+    body(std::true_type{});
   if constexpr (op_reduces(OP)) block_reduce_store<NACC>(acc, partials + (uint64_t)blockIdx.x * RED);
 }
 
@@ -471,13 +481,14 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
   constexpr bool TWO = (OP != DIAG_APPLY);
   cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
   const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  auto body = [&](auto guarded) __attribute__((always_inline)) {  // as k_direct
   for (uint32_t step = 0; step < g.it; step += U) {
     chunk fc[U], bc[U];
     bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = start + (uint64_t)(step + u) * BLOCK;
-      ok[u] = (step + u < g.it) && i < g.nchunks;
+      ok[u] = !decltype(guarded)::value || ((step + u < g.it) && i < g.nchunks);
       if (ok[u]) {
         fc[u] = ldc(f + (i + (i & g.gm)));
         if constexpr (TWO) bc[u] = ldc(b + (i + (i & g.gm)));
@@ -513,6 +524,11 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
       if constexpr (OP == DIAG_REVERSE || OP == DIAG_REVERSE_GRAD) stc(b + (i + (i & g.gm)), bc[u]);
     }
   }
+  };
+  if ((uint64_t)(blockIdx.x + 1) * BLOCK * g.it <= g.nchunks && g.it % U == 0)
+    body(std::false_type{});
+  else
+    body(std::true_type{});
   if constexpr (RED_) block_reduce_store<4>(acc, partials + (uint64_t)blockIdx.x * RED);
 }
 
