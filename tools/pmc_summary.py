@@ -7,7 +7,9 @@ FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane) coalesced stream
 every load of these kernels is a 16-byte nontemporal global_load_dwordx4 — so it is doubled.
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round>
+usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round> [--prefix P] [--detail-only]
+  --prefix P: the pass directories are P + pmc_FETCH_SIZE etc. (tools/gpu_f64.sh: f64_)
+  --detail-only: write <round>_pmc_traffic.json only (not the f32 pmc_traffic.json bench reads)
 """
 import csv
 import hashlib
@@ -67,11 +69,11 @@ def lib_sha16(precision="f32"):
     return hashlib.sha256((LIB / f"libqdc_{precision}.so").read_bytes()).hexdigest()[:16]
 
 
-def main(src, dst):
+def main(src, dst, prefix="", detail_only=False):
     src, dst = Path(src), Path(dst)
     dst.parent.mkdir(parents=True, exist_ok=True)
-    fetch, nf = per_launch(src / "pmc_FETCH_SIZE" / "pmc_counter_collection.csv", "FETCH_SIZE")
-    write, nw = per_launch(src / "pmc_WRITE_SIZE" / "pmc_counter_collection.csv", "WRITE_SIZE")
+    fetch, nf = per_launch(src / f"{prefix}pmc_FETCH_SIZE" / "pmc_counter_collection.csv", "FETCH_SIZE")
+    write, nw = per_launch(src / f"{prefix}pmc_WRITE_SIZE" / "pmc_counter_collection.csv", "WRITE_SIZE")
     traffic = {}
     for k in sorted(set(fetch) | set(write)):
         traffic[k] = round(fetch.get(k, 0.0) * 2 * 1024 + write.get(k, 0.0) * 1024)
@@ -79,6 +81,9 @@ def main(src, dst):
                   "launches_fetch_pass": nf.get(k), "launches_write_pass": nw.get(k),
                   "hbm_bytes_per_launch": traffic[k]} for k in traffic}
     (dst.parent / f"{dst.name}_pmc_traffic.json").write_text(json.dumps(detail, indent=1) + "\n")
+    if detail_only:
+        print(json.dumps(detail, indent=1))
+        return
     traffic["lib_sha16"] = lib_sha16()
     (dst.parent / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
     stats = src / "trace" / "trace_kernel_stats.csv"
@@ -93,4 +98,6 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    a = sys.argv[1:]
+    pre = a[a.index("--prefix") + 1] if "--prefix" in a else ""
+    main(a[0], a[1], pre, "--detail-only" in a)
