@@ -364,7 +364,8 @@ struct Circuit {
   // kernels at 64 % or 79 % of 8 TB/s from one circuit to the next (tools/alloc_probe.hip,
   // tools/pair_probe.hip, profiles/r2e_*, r2f_*).  Unsharded circuits only (a remap swaps the
   // states with the scratch buffer); QDC_STATE_ILV=0 keeps the plain layout (bwd separate and
-  // allocated on the first backward).
+  // allocated on the first backward).  The initial copy, the bwd zeroing and every gate-shaped
+  // kernel address the pair through Ctx::gm; readbacks copy block by block (read_state).
   const char* alloc_pair(Shard& s, size_t bytes) {
     const char* e = getenv("QDC_STATE_ILV");
     // states of at least two blocks (smaller ones gain nothing)
@@ -384,22 +385,11 @@ struct Circuit {
     }
     return nullptr;
   }
-  // geometry of one state of an interleaved pair as a 2-D copy: rows of 2^gap_bits chunks at a
-  // pitch of two rows
-  size_t ilv_width() const { return ((size_t)sizeof(cx) * VEC) << gap_bits; }
-  size_t ilv_rows() const { return nchunks_of(nl) >> gap_bits; }
-  const char* copy_initial(Shard& s) {
-    if (!gm) return elementwise<0>(s.c(), s.initial, s.state, nl);
-    QDC_HIP(hipMemcpy2DAsync(s.state, 2 * ilv_width(), s.initial, ilv_width(), ilv_width(),
-                             ilv_rows(), hipMemcpyDeviceToDevice, s.c().stream));
-    return nullptr;
-  }
+  // (kernels: a 2-D hipMemset / hipMemcpy over the 64 KiB blocks runs at < 1 TB/s)
+  const char* copy_initial(Shard& s) { return elementwise<0>(s.c(), s.initial, s.state, nl, gm); }
   const char* zero_bwd(Shard& s) {
-    if (!gm) {
-      QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));
-    } else {
-      QDC_HIP(hipMemset2DAsync(s.bwd, 2 * ilv_width(), 0, ilv_width(), ilv_rows(), s.c().stream));
-    }
+    if (gm) return elementwise<4>(s.c(), nullptr, s.bwd, nl, gm);
+    QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));
     return nullptr;
   }
   // host copy of amplitudes [offset, offset + len) of a (possibly interleaved) state

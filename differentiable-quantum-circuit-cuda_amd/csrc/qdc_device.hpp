@@ -568,16 +568,17 @@ inline const char* inject(Ctx& c, const cx* f, cx* b, const mat<R>& m, uint32_t 
   return run_op<OP_INJECT, R>(c, name, bytes, const_cast<cx*>(f), b, m, m, p, nullptr);
 }
 
-// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>
+// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>; op 4: 0.
+// gm: dst is a state of an interleaved pair (Ctx::gm), src plain
 template <int OP>
-inline const char* elementwise(Ctx& c, const cx* src, cx* dst, uint32_t n) {
+inline const char* elementwise(Ctx& c, const cx* src, cx* dst, uint32_t n, uint64_t gm = 0) {
   const uint64_t amps = (uint64_t)1 << n;
   const uint64_t nch = amps / VEC > 0 ? amps / VEC : 1;
   const uint32_t it = per_thread(nch, c.grid_cap);
   const uint32_t grid = (uint32_t)((nch + (uint64_t)BLOCK * it - 1) / ((uint64_t)BLOCK * it));
-  const double bytes = (OP == 2 ? 3.0 : OP == 3 ? 1.0 : 2.0) * state_bytes(n);
-  static const char* names[4] = {"copy", "conj_and_double", "add", "set_standard"};
-  return c.launch(names[OP], bytes, k_elementwise<OP>, grid, src, dst, amps, it);
+  const double bytes = (OP == 2 ? 3.0 : OP >= 3 ? 1.0 : 2.0) * state_bytes(n);
+  static const char* names[5] = {"copy", "conj_and_double", "add", "set_standard", "zero"};
+  return c.launch(names[OP], bytes, k_elementwise<OP>, grid, src, dst, amps, it, gm);
 }
 
 // the same kernels over an arbitrary number of complex values (reduction buffers)
@@ -586,7 +587,7 @@ inline const char* elementwise_count(Ctx& c, const cx* src, cx* dst, uint64_t co
   const uint64_t nch = count / VEC > 0 ? count / VEC : 1;
   const uint32_t it = per_thread(nch, c.grid_cap);
   const uint32_t grid = (uint32_t)((nch + (uint64_t)BLOCK * it - 1) / ((uint64_t)BLOCK * it));
-  return c.launch("reduce_sum", 0.0, k_elementwise<OP>, grid, src, dst, count, it);
+  return c.launch("reduce_sum", 0.0, k_elementwise<OP>, grid, src, dst, count, it, (uint64_t)0);
 }
 
 // remap pack of one shard of nl local qubits (victims: ascending amplitude positions >= 1)

@@ -1180,12 +1180,13 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
 
 // ---------------------------------------------------------------------------------------
 // Elementwise state kernels (primitives.cu:176-187, 879-939).
-// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>
+// op 0: dst = src; op 1: dst = 2 conj(src); op 2: dst += src; op 3: dst = |0..0>; op 4: dst = 0.
+// dst chunk i at i + (i & gm) (a state of an interleaved pair; src is always plain)
 // ---------------------------------------------------------------------------------------
 template <int OP>
 __global__ __launch_bounds__(BLOCK) void k_elementwise(const cx* __restrict__ src,
                                                        cx* __restrict__ dst, uint64_t n,
-                                                       uint32_t it) {
+                                                       uint32_t it, uint64_t gm) {
   const uint64_t nch = n / VEC;
   const chunk* s = reinterpret_cast<const chunk*>(src);
   chunk* d = reinterpret_cast<chunk*>(dst);
@@ -1193,10 +1194,11 @@ __global__ __launch_bounds__(BLOCK) void k_elementwise(const cx* __restrict__ sr
   for (uint32_t step = 0; step < it; ++step) {
     const uint64_t i = start + (uint64_t)step * BLOCK;
     if (i >= nch) break;
+    const uint64_t di = i + (i & gm);
     chunk a;
-    if constexpr (OP == 3) {
+    if constexpr (OP == 3 || OP == 4) {
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) a.v[v] = (i == 0 && v == 0) ? cx{1, 0} : cx{0, 0};
+      for (int v = 0; v < VEC; ++v) a.v[v] = (OP == 3 && i == 0 && v == 0) ? cx{1, 0} : cx{0, 0};
     } else {
       a = ldc(s + i);
     }
@@ -1204,16 +1206,16 @@ __global__ __launch_bounds__(BLOCK) void k_elementwise(const cx* __restrict__ sr
 #pragma unroll
       for (int v = 0; v < VEC; ++v) a.v[v] = {2 * a.v[v].x, -2 * a.v[v].y};
     } else if constexpr (OP == 2) {
-      const chunk o = ldc(d + i);
+      const chunk o = ldc(d + di);
 #pragma unroll
       for (int v = 0; v < VEC; ++v) a.v[v] = cadd(o.v[v], a.v[v]);
     }
-    stc(d + i, a);
+    stc(d + di, a);
   }
   // n < VEC (a 0-qubit state in f32): scalar tail
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     for (uint64_t k = nch * VEC; k < n; ++k) {
-      cx a = (OP == 3) ? cx{k == 0 ? (real)1 : (real)0, 0} : src[k];
+      cx a = (OP == 3) ? cx{k == 0 ? (real)1 : (real)0, 0} : (OP == 4) ? cx{0, 0} : src[k];
       if constexpr (OP == 1) a = {2 * a.x, -2 * a.y};
       if constexpr (OP == 2) a = cadd(dst[k], a);
       dst[k] = a;

@@ -43,6 +43,8 @@ def bench_name(kernel):
         return "fused_reverse" if m.group(1) == "true" else "fused_apply"
     if "k_elementwise<0>" in kernel:
         return "copy"
+    if "k_elementwise<4>" in kernel:
+        return "zero"
     if "k_finalize" in kernel:
         return "finalize"
     return None
