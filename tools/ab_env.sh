@@ -14,7 +14,7 @@ if [ -n "$TESTS" ]; then
 fi
 for r in $(seq 1 ${REPS:-1}); do
   for cfg in ${CFGS:--}; do
-    tag=$(echo "$cfg" | tr ',=/' '_--')
+    tag=$(echo "$cfg" | sed 's/[,=/]/_/g')
     envs=$( [ "$cfg" = "-" ] || echo "$cfg" | tr ',' ' ')
     env $envs timeout -k 10 300 python bench.py --steps ${STEPS_N:-3} --warmup 1 --no-cpu-baseline \
       --no-gate-sample ${BENCH_ARGS} > "$OUT/b_${tag}_$r.log" 2>&1 || { tail -5 "$OUT/b_${tag}_$r.log"; exit 1; }
