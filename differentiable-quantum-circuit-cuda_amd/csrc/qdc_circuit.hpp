@@ -239,6 +239,7 @@ struct Circuit {
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
   uint32_t rq_perm_low = 0;  // low positions a permuting pass fills, 0: default (QDC_RQ_PERM_LOW)
+  int rq_gstage = 1;  // two-state passes capped by Gamma stages, not variable gates (QDC_RQ_GSTAGE)
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -298,6 +299,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -368,10 +370,13 @@ struct Circuit {
   // kernel address the pair through Ctx::gm; readbacks copy block by block (read_state).
   const char* alloc_pair(Shard& s, size_t bytes) {
     const char* e = getenv("QDC_STATE_ILV");
-    // states of at least two blocks (smaller ones gain nothing)
-    const bool ilv = !(e && atoi(e) == 0) && g == 0 && sh.size() == 1 && nchunks_of(nl) >= 8192;
+    // block size: 2^12 chunks (QDC_STATE_ILV_BITS); states of at least two blocks
+    uint32_t gb = 12;
+    if (const char* b = getenv("QDC_STATE_ILV_BITS")) gb = (uint32_t)std::max(4, std::min(atoi(b), 24));
+    const bool ilv = !(e && atoi(e) == 0) && g == 0 && sh.size() == 1 &&
+                     nchunks_of(nl) >= ((uint64_t)2 << gb);
     if (ilv) {
-      gap_bits = 12;
+      gap_bits = gb;
       gm = ~(((uint64_t)1 << gap_bits) - 1);
       char* blk = nullptr;
       QDC_HIP(hipMalloc(&blk, 2 * bytes));
@@ -597,6 +602,7 @@ struct Circuit {
     P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
     P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
+    P.gamma_stage_cap = rq_gstage != 0;
     return P;
   }
   bool is_meas(const qdc_plan_op& op) const { return planner().is_meas(op); }

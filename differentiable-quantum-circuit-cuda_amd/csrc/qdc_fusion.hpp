@@ -81,6 +81,9 @@ struct FusionPlanner {
   bool permute = false;
   // two-state gate passes run register-resident (k_rq: FMAX_GRAD_RQ Gamma accumulators)
   bool rq_grad = false;
+  // ... and are capped by their Gamma STAGES (stages holding a variable gate: one accumulator
+  // each), not by their variable gates: a brickwork stage holds up to three of them
+  bool gamma_stage_cap = true;
   // low physical positions a permuting pass fills with the qubits the next ops need first
   // (>= NLOW; more makes the next tiles' contiguous runs longer)
   uint32_t perm_low = (uint32_t)LV + 3;
@@ -240,7 +243,9 @@ struct FusionPlanner {
              !(backward && j == first_inject && j > i))
         ++j;
       const bool two = backward && i >= first_inject;
-      const uint32_t gmax = (two && rq_grad) ? (uint32_t)FMAX_GRAD_RQ : (uint32_t)FMAX_GRAD;
+      const bool gstage = two && rq_grad && gamma_stage_cap;
+      const uint32_t gmax = gstage ? fuse_max_ops
+                            : (two && rq_grad) ? (uint32_t)FMAX_GRAD_RQ : (uint32_t)FMAX_GRAD;
       std::vector<uint32_t> rem;
       for (size_t k = i; k < j; ++k) rem.push_back((uint32_t)k);
       while (!rem.empty()) {
@@ -269,6 +274,21 @@ struct FusionPlanner {
           nred += isred;
           kind = (int)meas;
         }
+        // Gamma-stage cap: drop gates from the end of the pass (in pass order no kept gate
+        // depends on a dropped one) until its Gamma stages fit the accumulators
+        if (gstage && nred > (uint32_t)FMAX_GRAD_RQ) {
+          bool cut = false;
+          while (pass.size() > 1 && gamma_stages(pass, plan) > (uint32_t)FMAX_GRAD_RQ) {
+            rest.push_back(pass.back());
+            pass.pop_back();
+            cut = true;
+          }
+          if (cut) {
+            std::sort(rest.begin(), rest.end());
+            mask = 0;
+            for (uint32_t k : pass) mask |= op_bits(plan[k]);
+          }
+        }
         if (pass.size() == 1) {
           items.push_back(FusionItem{0, pass});
         } else {
@@ -284,6 +304,17 @@ struct FusionPlanner {
       i = j;
     }
     return items;
+  }
+
+  uint32_t gamma_stages(const std::vector<uint32_t>& pass,
+                        const std::vector<qdc_plan_op>& plan) const {
+    uint32_t n = 0;
+    for (const auto& st : stage_partition(pass, plan, true)) {
+      bool var = false;
+      for (uint32_t k : st) var = var || (plan[k].type == QDC_PLAN_OP && is_var(ins[plan[k].instr].kind));
+      n += var ? 1u : 0u;
+    }
+    return n;
   }
 
   // Split a pass (plan indices in pass order) into stages: greedy in program order, a gate
