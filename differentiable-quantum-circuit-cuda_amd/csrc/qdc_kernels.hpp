@@ -575,7 +575,10 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
 // (permlane swaps + DPP, ~V instructions for V values) and one LDS add per value into the
 // wave's accumulator slot; one partial per block and gradient stage at the end.
 // ---------------------------------------------------------------------------------------
-constexpr int FMAX_OPS = 32;   // gates per fused pass (>= its stages)
+#ifndef QDC_FMAX_OPS
+#define QDC_FMAX_OPS 32
+#endif
+constexpr int FMAX_OPS = QDC_FMAX_OPS;   // gates per fused pass (>= its stages)
 constexpr int FMAX_GRAD = 16;  // gradient gates per fused pass (>= its gradient stages)
 #ifndef QDC_FMAX_GRAD_RQ
 #define QDC_FMAX_GRAD_RQ 16
