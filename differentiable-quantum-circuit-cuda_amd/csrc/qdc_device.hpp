@@ -106,6 +106,9 @@ struct Ctx {
   // QDC_DIRECT_IT; 0: one item per thread).  tools/pair_probe.hip streams a far q1 pair at
   // 5.3 / 5.55 / 5.9 TB/s with 1 / 2 / 4 items per thread in flight
   uint32_t direct_it = 0;
+  // gates with no target at chunk bit 0..5 run on the TILE family too (far targets as row
+  // bits) instead of the direct rows (knob QDC_TILE_FAR: bit 0 two-state ops, bit 1 one-state)
+  uint32_t tile_far = 0;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -126,6 +129,7 @@ struct Ctx {
     if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_TILE_FAR")) tile_far = (uint32_t)atoi(e);
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
@@ -249,12 +253,12 @@ inline uint32_t per_thread(uint64_t items, uint32_t target) {
 
 // q1: R = 2, pos2 == pos1 == target.  q2: R = 4.
 inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_states,
-                      uint32_t grid_target) {
+                      uint32_t grid_target, bool far_tile = false) {
   Plan p;
   p.R = R;
   const uint64_t nch = nchunks_of(n);
   const bool low = is_low(pos1) || (R == 4 && is_low(pos2));
-  if (!low) {
+  if (!low && !far_tile) {
     if (R == 2) {
       if ((int)pos1 < LV) {
         p.mode = 1;
@@ -290,24 +294,30 @@ inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_
   const uint32_t T = two_states ? 9 : 10;
   const uint32_t cbits = log2u(nch);
   const uint32_t teff = cbits < T ? cbits : T;
-  uint32_t l = teff, h = 0, hb0 = 0;
-  if (R == 4) {
-    // the non-low target may lie beyond the tile's contiguous bits: make it a row bit
-    const uint32_t far = is_low(pos1) ? pos2 : pos1;
-    if (far >= (uint32_t)LV && far - LV >= teff) {
-      h = 1;
-      l = teff - 1;
-      hb0 = far - LV;
-    }
+  // targets at chunk bits beyond the tile's contiguous bits become row bits (each row bit
+  // takes one contiguous bit, which may push a second target out: iterate)
+  const uint32_t tq[2] = {pos1, pos2};
+  const int nt = (R == 2) ? 1 : 2;
+  uint32_t l = teff, h = 0, hb[2] = {0, 0};
+  for (;;) {
+    uint32_t k = 0, fb[2] = {0, 0};
+    for (int i = 0; i < nt; ++i)
+      if (tq[i] >= (uint32_t)LV && tq[i] - LV >= teff - h) fb[k++] = tq[i] - LV;
+    if (k <= h) break;
+    h = k;
+    hb[0] = fb[0] < fb[1] || k == 1 ? fb[0] : fb[1];
+    hb[1] = k == 1 ? 0 : (fb[0] < fb[1] ? fb[1] : fb[0]);
   }
+  l = teff - h;
+  const uint32_t hb0 = hb[0];
   auto local_bit = [&](uint32_t q) -> uint32_t {
     if (q < (uint32_t)LV || q - LV < l) return q;
-    return LV + l;  // row bit 0
+    return (q - LV == hb0) ? LV + l : LV + l + 1;  // row bit 0 / 1
   };
   p.tg.l = l;
   p.tg.h = h;
   p.tg.hb0 = hb0;
-  p.tg.hb1 = 0;
+  p.tg.hb1 = hb[1];
   p.tg.t1 = local_bit(pos1);
   p.tg.t2 = local_bit(pos2);
   p.tg.ntiles = nch >> (l + h);
@@ -442,7 +452,8 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
 template <int R>
 inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
                      bool reduces) {
-  Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap);
+  Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
+                     (c.tile_far >> (two ? 0 : 1)) & 1u);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
