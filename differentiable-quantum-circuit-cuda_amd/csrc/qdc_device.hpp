@@ -107,8 +107,12 @@ struct Ctx {
   // 5.3 / 5.55 / 5.9 TB/s with 1 / 2 / 4 items per thread in flight
   uint32_t direct_it = 0;
   // gates with no target at chunk bit 0..5 run on the TILE family too (far targets as row
-  // bits) instead of the direct rows (knob QDC_TILE_FAR: bit 0 two-state ops, bit 1 one-state)
-  uint32_t tile_far = 0;
+  // bits) instead of the direct rows.  Knob QDC_TILE_FAR, one bit per op class: bit 0 reverse
+  // (both states read and written), bit 1 one-state ops, bit 2 inject / grad.  Measured at
+  // n = 28 (profiles/r2m_micro_table_tf*.txt): reverse_q1 68-70 -> 75-77 % of 8 TB/s at every
+  // far position, reverse_q2 (14,13) 65.7 -> 69.6 %; one-state apply 77 -> 68 % and inject
+  // 79 -> 71 % at some positions, so only bit 0 is on
+  uint32_t tile_far = 1;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -451,9 +455,10 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
 
 template <int R>
 inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
-                     bool reduces) {
+                     bool reduces, bool writes_both = false) {
+  const uint32_t cls = writes_both ? 0u : two ? 2u : 1u;  // QDC_TILE_FAR bit
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
-                     (c.tile_far >> (two ? 0 : 1)) & 1u);
+                     (c.tile_far >> cls) & 1u);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
@@ -541,12 +546,12 @@ inline const char* reverse_dense(Ctx& c, cx* f, cx* b, const mat<R>& A, const ma
   const double bytes = 4.0 * state_bytes(n);
   const char* name = (R == 2) ? "reverse_q1" : "reverse_q2";
   if (grad_base) {
-    const Plan p = plan_for<R>(c, n, pos2, pos1, true, true);
+    const Plan p = plan_for<R>(c, n, pos2, pos1, true, true, true);
     return reduce_into(c, grad_base, dst, 0, blocks_of(p), [&](cx* out) {
       return run_op<OP_REVERSE_GRAD, R>(c, name, bytes, f, b, A, B, p, out);
     });
   }
-  const Plan p = plan_for<R>(c, n, pos2, pos1, true, false);
+  const Plan p = plan_for<R>(c, n, pos2, pos1, true, false, true);
   return run_op<OP_REVERSE, R>(c, name, bytes, f, b, A, B, p, nullptr);
 }
 

@@ -209,13 +209,15 @@ def test_register_resident_passes_equal_lds_passes(case):
                          f"{case} {name} vs lds grads")
 
 
-@pytest.mark.parametrize("n,perm_low", [(13, 0), (18, 0), (18, 6), (18, 8)])
-def test_permuting_passes_equal_fixed_layout(n, perm_low):
+@pytest.mark.parametrize("n,perm_low,lcmin",
+                         [(13, 0, 0), (18, 0, 0), (18, 6, 0), (18, 8, 0), (18, 5, 4), (18, 6, 5)])
+def test_permuting_passes_equal_fixed_layout(n, perm_low, lcmin):
     """f32 gate-only passes permute their tile's qubits on the way out (QDC_RQ_PERM=1, the
     default; later ops run at rewritten positions).  Densities, gradients and the forward and
     uncomputed states (read back in logical order) equal the fixed-layout run and the oracle.
     QDC_RQ_PERM_LOW (low positions a permuting pass fills; 0 = the default LV + 3) 6 and 8 move
-    qubits to tile bits >= 4, stored through the dest-mapped layout (qdc_fusion.hpp rq_hbm)."""
+    qubits to tile bits >= 4, stored through the dest-mapped layout (qdc_fusion.hpp rq_hbm);
+    with QDC_FUSE_LCMIN 4 / 5 (256-B / 512-B tile rows) those bits are contiguous chunk bits."""
     ins, var = O.layered_circuit(n, 5, seed=n)
     fl = F.Floor("f32", n, ins, [], var, run=False)
     res = {}
@@ -223,6 +225,8 @@ def test_permuting_passes_equal_fixed_layout(n, perm_low):
         env = {"QDC_RQ_PERM": perm, "QDC_FUSE": 1}
         if perm_low:
             env["QDC_RQ_PERM_LOW"] = perm_low
+        if lcmin:
+            env["QDC_FUSE_LCMIN"] = lcmin
         c = build_env("f32", n, ins, env)
         d = c.forward([], fl.var)
         fwd_state = c.get_state(0)
@@ -232,7 +236,7 @@ def test_permuting_passes_equal_fixed_layout(n, perm_low):
     assert res[1][4] != list(range(n))  # the permuting run did leave a permuted layout
     for perm in (0, 1):
         d, g, fs, us, _ = res[perm]
-        what = f"layered n={n} perm={perm} perm_low={perm_low} "
+        what = f"layered n={n} perm={perm} perm_low={perm_low} lcmin={lcmin} "
         fl.check("forward", d, what)
         fl.check("grads", g, what)
         fl.check("state", fs, what)

@@ -84,3 +84,39 @@ def test_interleaved_range_reads(prec):
         assert np.array_equal(np.concatenate(parts), full), f"state {which}"
         mid = c.get_range(which, blk // 2, 2 * blk + 3)
         assert np.array_equal(mid, full[blk // 2: blk // 2 + 2 * blk + 3])
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_far_target_tile_plans(prec):
+    """QDC_TILE_FAR (qdc_device.hpp plan_gate): single-gate ops with no target at chunk bits
+    0..5 run on the tile family with every far target as a row bit (reverse ops by default,
+    bit 0), or on the direct rows.  n = 17 puts most positions beyond a tile's contiguous bits
+    and q2 pairs with one or two far targets.  Every op class on either family (0: all direct,
+    7: all tiled) matches the oracle within the measured floors, and the two runs agree."""
+    n = 17
+    ins, const, var = O.random_circuit(n, 120, seed=41, density_every=30)
+    psi0 = O.random_state(np.random.default_rng(8), n)
+    fl = F.Floor(prec, n, ins, const, var, psi0=psi0, cots=F.tsallis_cots, run=False)
+    res = {}
+    for tf in (0, 7):
+        old = os.environ.get("QDC_TILE_FAR")
+        os.environ["QDC_TILE_FAR"] = str(tf)
+        try:
+            c = build(prec, n, ins, 1, fuse=0)
+        finally:
+            if old is None:
+                del os.environ["QDC_TILE_FAR"]
+            else:
+                os.environ["QDC_TILE_FAR"] = old
+        c.set_state_from_vector(fl.psi0)
+        d = c.forward(fl.const, fl.var)
+        fwd = c.get_state(0)
+        g = c.backward(fl.cots, fl.const, fl.var)
+        what = f"tile_far={tf} n={n} {prec} "
+        fl.check("forward", d, what)
+        fl.check("state", fwd, what)
+        fl.check("grads", g, what)
+        fl.check("uncomputed", c.get_state(0), what)
+        res[tf] = g
+        del c
+    F.check_pair(prec, res[7], res[0], fl.floor["grads"], f"n={n} {prec} tiled vs direct grads")
