@@ -61,7 +61,7 @@ inline void qk_operands(const cx* U, std::vector<real>& a) {
 // whose amplitudes at each offset form one 16-B chunk — every load and store is 16 B per lane
 // (256 contiguous bytes per quad) and each batch runs the MFMA chain twice.  P = 1: one group
 // per lane, 8-B (f32) accesses.
-template <int K, int P>
+template <int K, int P, int NB>
 __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __restrict__ aop,
                                             qk_geo g) {
   constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
@@ -82,8 +82,6 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
 #pragma unroll
   for (int m = 0; m < M; ++m) off[m] = g.off[M * q + m];
   // NB batches of 16 P groups per iteration, all loads first (bytes in flight per wave)
-  constexpr int NB0 = K == 3 ? 4 : K == 4 ? 2 : 1;
-  constexpr int NB = NB0;
   constexpr uint64_t GB = 16 * P;  // groups per batch
   const uint64_t nbatch = (g.ngroups + GB - 1) / GB;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -217,8 +215,12 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   // at n = 28 (tools/qk_probe.py): k = 3 +5-7 %, k = 5 +5 %, k = 4 -10 % (kept at 8 B)
   bool pair = sizeof(real) == 4 && g.sorted[0] != 0 && k != 4;
   if (const char* ev = getenv("QDC_QK_PAIR")) pair = pair && atoi(ev) != 0;
-  const uint64_t nb0 = k == 3 ? 4 : k == 4 ? 2 : 1;  // batches per wave iteration (k_qk)
-  const uint64_t nb = nb0;
+  // batches per wave iteration (k_qk NB): 4 / 2 / 1 at k = 3 / 4 / 5, doubled ("wide": more
+  // bytes in flight per wave) at k >= 4 — measured at n = 28 (tools/qk_probe.py,
+  // profiles/r2o_qk_probe.log): k = 3 neutral, k = 4 +2 %, k = 5 +7 %.  Knob QDC_QK_WIDE=0/1
+  const char* ew = getenv("QDC_QK_WIDE");
+  const bool wide = ew ? atoi(ew) != 0 : k >= 4;
+  const uint64_t nb = (k == 3 ? 4 : k == 4 ? 2 : 1) * (wide ? 2 : 1);
   const uint64_t gpb = pair ? 32 : 16;  // groups per batch
   const uint64_t waves = ((g.ngroups + gpb - 1) / gpb + nb - 1) / nb;
   const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 256u * 16u);
@@ -226,16 +228,20 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   const double bytes = 2.0 * state_bytes(n);
   const real* buf = ring.dev[slot];
   const char* e;
+#define QDC_QK_LAUNCH(KK, PP, NB3)                                                              \
+  e = wide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3)>, grid, 256u, s, buf, g)     \
+           : c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3)>, grid, 256u, s, buf, g)
 #ifndef QDC_F64
   if (pair) {
-    if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3, 2>, grid, 256u, s, buf, g);
-    else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4, 2>, grid, 256u, s, buf, g);
-    else e = c.launch_block("qk5", bytes, k_qk<5, 2>, grid, 256u, s, buf, g);
+    if (k == 3) QDC_QK_LAUNCH(3, 2, 4);
+    else if (k == 4) QDC_QK_LAUNCH(4, 2, 2);
+    else QDC_QK_LAUNCH(5, 2, 1);
   } else
 #endif
-  if (k == 3) e = c.launch_block("qk3", bytes, k_qk<3, 1>, grid, 256u, s, buf, g);
-  else if (k == 4) e = c.launch_block("qk4", bytes, k_qk<4, 1>, grid, 256u, s, buf, g);
-  else e = c.launch_block("qk5", bytes, k_qk<5, 1>, grid, 256u, s, buf, g);
+  if (k == 3) QDC_QK_LAUNCH(3, 1, 4);
+  else if (k == 4) QDC_QK_LAUNCH(4, 1, 2);
+  else QDC_QK_LAUNCH(5, 1, 1);
+#undef QDC_QK_LAUNCH
   QDC_TRY(e);
   QDC_HIP(hipEventRecord(ring.done[slot], c.stream));
   return nullptr;
