@@ -358,6 +358,19 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   return items.size();
 }
 
+QDC_API int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1,
+                          int two_states, int far_tile, unsigned* out) {
+  if (!out || (R != 2 && R != 4) || n < 2 || n > 62 || pos2 >= n || pos1 >= n ||
+      (R == 2 && pos2 != pos1) || (R == 4 && pos2 == pos1))
+    return -1;
+  const qdc::Plan p = qdc::plan_gate(n, (int)R, pos2, pos1, two_states != 0, 1024u, far_tile != 0);
+  const uint64_t cnt = p.tile ? p.tg.ntiles : p.g.items;
+  const unsigned v[10] = {p.tile ? 1u : 0u, (unsigned)p.mode, p.tg.l, p.tg.h, p.tg.hb0, p.tg.hb1,
+                          p.tg.t1, p.tg.t2, (unsigned)(cnt & 0xffffffffu), (unsigned)(cnt >> 32)};
+  for (int i = 0; i < 10; ++i) out[i] = v[i];
+  return 0;
+}
+
 QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds,
                            const unsigned* t1, const unsigned* t2,
                            const unsigned long long* deps, size_t n, unsigned* steps,

@@ -200,6 +200,15 @@ size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds, co
                    const unsigned* t2, const unsigned long long* deps, size_t n,
                    unsigned* steps, size_t cap);
 
+/* Test hook (host only): the launch geometry a single-gate op gets (qdc_device.hpp plan_gate)
+ * on an n-qubit state: R = 2 (one-qubit, pos2 == pos1) or 4; two_states: the op reads both
+ * states (tile of 2^9 chunks, else 2^10); far_tile: targets beyond chunk bit 5 go to the tile
+ * family as row bits too (QDC_TILE_FAR).  out[0..9] = {tile, mode (direct), l, h, hb0, hb1,
+ * t1, t2, ntiles (tile) or items (direct) low 32 bits, high 32 bits}.  Returns 0, or -1 on
+ * invalid arguments. */
+int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int two_states,
+                  int far_tile, unsigned* out);
+
 #ifdef __cplusplus
 }
 #endif
