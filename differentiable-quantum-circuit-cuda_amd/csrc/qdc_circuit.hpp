@@ -232,7 +232,9 @@ struct Circuit {
   int rq64 = 1;  // f64 gate passes register-resident too (k_rw; QDC_RQ64)
   int rq_slots5 = 1;  // two-state f32 k_rw passes plan five register slots (QDC_RQ_SLOTS5)
   bool rq5() const { return rq_slots5 != 0 && (rq_wave & 1) && !(rq_wave & 4); }
-  int rq_order = 0;  // register-resident tile order: 0 block-contiguous, 1 grid-strided (QDC_RQ_ORDER)
+  // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
+  // XCD-aware block order (QDC_RQ_ORDER)
+  int rq_order = 0;
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)

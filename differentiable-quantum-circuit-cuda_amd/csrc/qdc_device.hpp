@@ -113,6 +113,11 @@ struct Ctx {
   // far position, reverse_q2 (14,13) 65.7 -> 69.6 %; one-state apply 77 -> 68 % and inject
   // 79 -> 71 % at some positions, so only bit 0 is on
   uint32_t tile_far = 1;
+  // XCD-aware block order of streaming single-gate launches (direct and tile families; knob
+  // QDC_XCD_MAP): the blocks one XCD runs own adjacent ranges.  Measured at n = 28
+  // (profiles/r2t_micro_table_xcd*.txt): injections at q1 1..6 71 -> 76 %, apply/inject at
+  // q1 7..11 and 21..23 +4..7 points, apply_q2 71.6 -> 73.4 %; q1 24 71.8 -> 69.4 %
+  uint32_t xcd_map = 1;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -134,6 +139,7 @@ struct Ctx {
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE_FAR")) tile_far = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_XCD_MAP")) xcd_map = (uint32_t)atoi(e);
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
@@ -460,6 +466,9 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
                      (c.tile_far >> cls) & 1u);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
+  // XCD-aware order for streaming launches only: reductions (few long-lived blocks with
+  // contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
+  p.g.xcd = p.tg.xcd = reduces ? 0u : c.xcd_map;
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
   return p;

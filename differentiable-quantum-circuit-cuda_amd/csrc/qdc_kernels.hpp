@@ -210,8 +210,17 @@ struct geo {
   uint32_t lo;     // chunk bit positions for zero insertion (lower first)
   uint32_t hi;
   uint32_t it;     // items per thread (block-contiguous iteration)
+  uint32_t xcd;    // 1: XCD-aware block order (the blocks one XCD runs own adjacent ranges)
   uint64_t gm;     // gap mask: chunk c of a state lives at c + (c & gm) (interleaved pair)
 };
+
+// Blocks are dispatched round-robin over the 8 XCDs (block b on XCD b % 8).  The XCD-aware
+// order gives XCD x the contiguous block range [x G/8, (x+1) G/8) (G a multiple of 8, else
+// the identity), so each XCD streams its own part of the state.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t grid, uint32_t on) {
+  if (!on || (grid & 7u)) return b;
+  return (b & 7u) * (grid >> 3) + (b >> 3);
+}
 
 template <int R, int MODE>
 struct rows {
@@ -290,7 +299,8 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
   cx acc[NACC];
 #pragma unroll
   for (int k = 0; k < NACC; ++k) acc[k] = {0, 0};
-  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, g.xcd);
+  const uint64_t start = (uint64_t)blk * BLOCK * g.it + threadIdx.x;
   // blocks whose items all exist (every block of a power-of-two state) run without per-item
   // guards: a guarded load is a branch the waitcnt pass drains in-flight loads around
   auto body = [&](auto guarded) __attribute__((always_inline)) {
@@ -334,7 +344,7 @@ __global__ __launch_bounds__(BLOCK) void k_direct(chunk* __restrict__ f, chunk* 
     }
   }
   };
-  if ((uint64_t)(blockIdx.x + 1) * BLOCK * g.it <= g.items && g.it % U == 0)
+  if ((uint64_t)(blk + 1) * BLOCK * g.it <= g.items && g.it % U == 0)
     body(std::false_type{});
   else
     body(std::true_type{});
@@ -355,6 +365,7 @@ struct tgeo {
   uint32_t h;      // row bits (0..2)
   uint32_t hb0, hb1;  // global chunk bit of row bit 0 / 1
   uint32_t t1, t2;    // tile-local amplitude bits of the gate's index bits 0 (pos1) and 1 (pos2)
+  uint32_t xcd;       // XCD-aware block order (geo::xcd)
   uint64_t gm;        // gap mask (geo::gm)
 };
 
@@ -387,7 +398,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
   const uint32_t ng = (tc * VEC) / R;          // gate groups per tile
   const uint32_t lo_t = tg.t1 < tg.t2 ? tg.t1 : tg.t2;
   const uint32_t hi_t = tg.t1 < tg.t2 ? tg.t2 : tg.t1;
-  const uint64_t tile0 = (uint64_t)blockIdx.x * tg.tpb;
+  const uint64_t tile0 = (uint64_t)xcd_block(blockIdx.x, gridDim.x, tg.xcd) * tg.tpb;
   for (uint32_t tt = 0; tt < tg.tpb; ++tt) {
     const uint64_t tile = tile0 + tt;
     if (tile >= tg.ntiles) break;

@@ -443,8 +443,9 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   }
   // block-contiguous tiles (tile0 + s) or grid-strided (tile0 + s * grid: concurrently running
   // tiles are neighbours in memory)
-  const bool gstride = fg.order != 0;
-  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * fg.tpb;
+  const bool gstride = fg.order == 1;  // 2: block-contiguous in XCD-aware block order
+  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x
+                                 : (uint64_t)xcd_block(blockIdx.x, gridDim.x, fg.order == 2) * fg.tpb;
   const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
   const uint32_t count =
       tile0 >= fg.ntiles ? 0u
@@ -659,8 +660,9 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   }
   // block-contiguous tiles (tile0 + s) or grid-strided (tile0 + s * grid: concurrently running
   // tiles are neighbours in memory)
-  const bool gstride = fg.order != 0;
-  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * fg.tpb;
+  const bool gstride = fg.order == 1;  // 2: block-contiguous in XCD-aware block order
+  const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x
+                                 : (uint64_t)xcd_block(blockIdx.x, gridDim.x, fg.order == 2) * fg.tpb;
   const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
   const uint32_t count =
       tile0 >= fg.ntiles ? 0u

@@ -166,7 +166,8 @@ def build_env(prec, n, ins, env):
 
 # register-resident variants (csrc/qdc_rq.hpp): k_rq (a tile per block of NT threads, QDC_RW=0),
 # k_rw (a tile per wave; bit 0 two-state, bit 1 one-state, bit 2 two-state with the next tile
-# prefetched into AGPRs), and the grid-strided tile order
+# prefetched into AGPRs), the grid-strided tile order, and block-contiguous tiles in XCD-aware
+# block order
 RQ_VARIANTS = {
     "lds": {"QDC_RQ": 0},
     "k_rq": {"QDC_RQ": 1, "QDC_RW": 0},
@@ -174,6 +175,7 @@ RQ_VARIANTS = {
     "k_rw_all": {"QDC_RQ": 1, "QDC_RW": 3},
     "k_rw_pf": {"QDC_RQ": 1, "QDC_RW": 5},
     "k_rw_gstride": {"QDC_RQ": 1, "QDC_RW": 1, "QDC_RQ_ORDER": 1},
+    "k_rw_xcd": {"QDC_RQ": 1, "QDC_RW": 1, "QDC_RQ_ORDER": 2},
 }
 
 
