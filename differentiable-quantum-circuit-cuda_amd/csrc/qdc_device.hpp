@@ -466,9 +466,9 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
                      (c.tile_far >> cls) & 1u);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
-  // XCD-aware order for streaming launches only: reductions (few long-lived blocks with
-  // contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
-  p.g.xcd = p.tg.xcd = reduces ? 0u : c.xcd_map;
+  // XCD-aware order for streaming launches only by default: reductions (few long-lived blocks
+  // with contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
+  p.g.xcd = p.tg.xcd = (c.xcd_map >> (reduces ? 1 : 0)) & 1u;  // bit 0 streaming, 1 reducing
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
   return p;
