@@ -123,6 +123,9 @@ struct Ctx {
   // (profiles/r2y_micro_table_tile2_wide*.txt): reverse_q2 +1.2..3.3 points on every pair
   // ((26,27) 66.3 -> 69.6 %, (14,13) 69.4 -> 71.4 %), reverse_q1 and injections within +-0.5
   uint32_t tile2_wide = 1;
+  // one-state tile-family launches on 2^11-chunk tiles (K = 8, 32 KiB of LDS) instead of 2^10
+  // (knob QDC_TILE1_WIDE)
+  uint32_t tile1_wide = 0;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -146,6 +149,7 @@ struct Ctx {
     if (const char* e = getenv("QDC_TILE_FAR")) tile_far = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_XCD_MAP")) xcd_map = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE2_WIDE")) tile2_wide = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_TILE1_WIDE")) tile1_wide = (uint32_t)atoi(e);
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
@@ -269,7 +273,8 @@ inline uint32_t per_thread(uint64_t items, uint32_t target) {
 
 // q1: R = 2, pos2 == pos1 == target.  q2: R = 4.
 inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_states,
-                      uint32_t grid_target, bool far_tile = false, bool wide2 = false) {
+                      uint32_t grid_target, bool far_tile = false, bool wide2 = false,
+                      bool wide1 = false) {
   Plan p;
   p.R = R;
   const uint64_t nch = nchunks_of(n);
@@ -307,7 +312,8 @@ inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_
   }
   // TILE: 256*K chunks per state per tile, K = 4 (one state) or 2 (two states)
   p.tile = true;
-  const uint32_t T = two_states && !wide2 ? 9 : 10;  // wide2: two-state tiles of 2^10 chunks
+  // wide2: two-state tiles of 2^10 chunks; wide1: one-state tiles of 2^11
+  const uint32_t T = two_states ? (wide2 ? 10 : 9) : (wide1 ? 11 : 10);
   const uint32_t cbits = log2u(nch);
   const uint32_t teff = cbits < T ? cbits : T;
   // targets at chunk bits beyond the tile's contiguous bits become row bits (each row bit
@@ -454,6 +460,8 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
     constexpr int K = op_two_states(OP) ? 2 : 4;
     if (K == 2 && p.tg.l + p.tg.h > 9)  // a wide two-state tile (QDC_TILE2_WIDE)
       return c.launch(name, bytes, k_tile<OP, R, 4>, grid, fc, bc, A, B, p.tg, partials);
+    if (K == 4 && p.tg.l + p.tg.h > 10)  // a wide one-state tile (QDC_TILE1_WIDE)
+      return c.launch(name, bytes, k_tile<OP, R, 8>, grid, fc, bc, A, B, p.tg, partials);
     return c.launch(name, bytes, k_tile<OP, R, K>, grid, fc, bc, A, B, p.tg, partials);
   }
   if (p.mode == 0)
@@ -472,7 +480,7 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
                      bool reduces, bool writes_both = false) {
   const uint32_t cls = writes_both ? 0u : two ? 2u : 1u;  // QDC_TILE_FAR bit
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
-                     (c.tile_far >> cls) & 1u, c.tile2_wide != 0);
+                     (c.tile_far >> cls) & 1u, c.tile2_wide != 0, c.tile1_wide != 0);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   // XCD-aware order for streaming launches only by default: reductions (few long-lived blocks
   // with contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
