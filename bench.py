@@ -13,7 +13,8 @@ value = gates x steps / wall time (every gate is applied once forward and once i
 reverse sweep); inputs are resident in HBM before the timed region (gate matrices are 16-256 B
 host arrays passed per call, as in the reference API).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): strong scaling — the SAME
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N, torch only as the launcher):
+strong scaling — the SAME
 n-qubit state is sharded over the N GPUs by its high qubits; gates on a global
 qubit trigger a remap (pack + one RCCL all-to-all over xGMI), densities and gradients are
 all-reduced.  value = the circuit's gates x steps / (max over ranks of the wall time).
@@ -54,6 +55,8 @@ def parse():
                     help="gates of the CPU baseline sample (the workload's first gates, full n)")
     ap.add_argument("--cpu-densities", type=int, default=4)
     ap.add_argument("--cpu-qubits", type=int, default=None)
+    ap.add_argument("--cpu-c3-max-s", type=float, default=120.0,
+                    help="time one whole C3 call on the CPU when its projection is below this")
     ap.add_argument("--pmc", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--micro", action="store_true", help="per-kernel bandwidth sweep")
     return ap.parse_args()
@@ -76,39 +79,23 @@ def sigma_z_cotangents(ndens, dt):
 
 
 def dist_setup(args):
+    """One process per GPU under any launcher that exports WORLD_SIZE / RANK / LOCAL_RANK
+    (torch.distributed.run here, as the driver launches it): the ranks coordinate only through
+    the circuit's own RCCL communicator (quantum_differentiable_circuit.distributed), so no
+    second collective stack (torch's bundled RCCL, gloo) is loaded into the process."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
     return world, rank, local
 
 
-def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+def barrier(comm):
+    if comm is not None and comm.world > 1:
+        comm.barrier()
 
 
-def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def max_over_ranks(x, comm):
+    return comm.max(x) if comm is not None and comm.world > 1 else x
 
 
 def select_device(local):
@@ -187,6 +174,25 @@ def _cref_op_costs(ops, n, q1_pos, q2_pairs, dens1_pos, dens2_pairs, diag_pairs=
     return out
 
 
+def _cref_whole_call(ops, n, circuit, dt, psi0=None, cot=None):
+    """Wall time of one forward + backward call of the reference algorithm
+    (oracle.OracleCircuit: circuit.rs:164-429 driving the C kernels) on a whole circuit."""
+    from oracle import oracle as O
+    ins, var = circuit
+    o = O.OracleCircuit(n, dt, ops=ops)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    if psi0 is not None:
+        o.set_state_from_vector(psi0)
+    vg = [np.ascontiguousarray(g, dtype=ops.state_dtype) for g in var]
+    t0 = time.perf_counter()
+    dens = o.forward([], vg)
+    cots = [np.ascontiguousarray(cot if cot is not None else np.diag([1.0, -1.0]), dtype=dt)
+            for _ in dens]
+    o.backward(cots, [], vg)
+    return {"s": time.perf_counter() - t0, "ins": ins}
+
+
 def cpu_baseline(args, n):
     """The reference's algorithm on the host cores (oracle/cpu_ref.c: its CUDA kernels'
     index rules in C/OpenMP, driven in circuit.rs's order: unfused, one kernel per step, a new
@@ -230,6 +236,37 @@ def cpu_baseline(args, n):
     res["c3_vqse"] = {"s_per_loss_grad_call": round(call, 2), "qubits": n3, "layers": layers3,
                       "dtype": "c128 (f64)", "cores": ops64.threads(),
                       "per_gate_s": {k: round(v, 4) for k, v in c3.items()}}
+    # validation of the projections: whole calls of the reference algorithm, timed end to end
+    # (oracle.OracleCircuit = circuit.rs:164-429 over the C kernels; one C2 layer with its 28
+    # densities at full n, and one whole C3 loss-and-gradient call when its projection is short)
+    res["measured"] = measured = {}
+    try:
+        m = _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), np.complex64
+                             if args.precision == "f32" else np.complex128)
+        l_q1 = sum(1 for k, _ in m["ins"] if k == 8)
+        l_q2 = sum(1 for k, _ in m["ins"] if k == 1)
+        l_d1 = sum(1 for k, _ in m["ins"] if k == 13)
+        proj = l_q1 * c2["q1"] + l_q2 * c2["q2"] + l_d1 * c2["dens1"]
+        measured["c2_one_layer"] = {
+            "measured_layer_s": round(m["s"], 2), "projected_s": round(proj, 2),
+            "projection_error": round((proj - m["s"]) / m["s"], 4),
+            "gates": l_q1 + l_q2, "densities": l_d1, "qubits": n, "threads": threads}
+    except Exception as e:  # noqa: BLE001
+        measured["c2_one_layer"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if call <= args.cpu_c3_max_s:
+        try:
+            p = np.random.default_rng(42).normal(size=2 * layers3)
+            ins3 = W.vqse_ising(n3, layers3)
+            gates3 = W.vqse_gates(p, n3)
+            psi3 = np.full(1 << n3, 1.0 / np.sqrt(1 << n3), np.complex128)
+            m3 = _cref_whole_call(ops64, n3, (ins3, gates3), np.complex128, psi0=psi3,
+                                  cot=W.tfim_term(1.0).T.conj())
+            res["c3_vqse"].update({"measured_call_s": round(m3["s"], 2),
+                                   "projection_error": round((call - m3["s"]) / m3["s"], 4)})
+        except Exception as e:  # noqa: BLE001
+            res["c3_vqse"]["measured_error"] = f"{type(e).__name__}: {e}"[:300]
+    else:
+        res["c3_vqse"]["measured_call_s"] = f"skipped: projected {call:.0f} s > --cpu-c3-max-s"
     wall = time.perf_counter() - t_all
     return {"value": round((n_q1 + n_q2) / step, 4), "unit": "gate-applications/s (fwd+bwd)",
             "cores": threads, "kind": "port", "s_per_step": round(step, 2),
@@ -239,7 +276,10 @@ def cpu_baseline(args, n):
                        f"{len(spread)} positions, q2 at {len(spread)} pairs, q1 density+injection at 2; "
                        f"projected onto C2's {n_q1} q1 + {n_q2} q2 gates + {n_d1} densities per "
                        f"step; single_thread: one position per kind; c3_vqse: n=26 f64 diagonal, "
-                       f"q1 and q2-density costs projected onto 26 layers; {wall:.0f} s of CPU time"),
+                       f"q1 and q2-density costs projected onto 26 layers; measured: one whole C2 "
+                       f"layer (its gates and densities, fwd+bwd, circuit.rs order) and one whole "
+                       f"C3 call timed end to end against their projections; {wall:.0f} s of CPU "
+                       f"time"),
             **res}
 
 
@@ -503,7 +543,7 @@ def main():
     c.synchronize()
 
     c.profile(True)
-    barrier(world)
+    barrier(comm)
     c.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -511,11 +551,11 @@ def main():
         grads = c.backward(cots, [], vg)
     c.synchronize()
     elapsed = time.perf_counter() - t0
-    barrier(world)
+    barrier(comm)
     stats = c.profile_collect()
     c.profile(False)
 
-    elapsed = max_over_ranks(elapsed, world)
+    elapsed = max_over_ranks(elapsed, comm)
     value = ngates * args.steps / elapsed  # the one sharded circuit's gate applications
 
     # dominant HBM kernel = the one with the largest share of measured device time
@@ -633,9 +673,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@ QDC_API const char* qdc_circuit_new(qdc_circuit** out, size_t qubits_number) {
 }
 
 QDC_API void qdc_circuit_free(qdc_circuit* c) {
+  qdc::DeviceGuard keep;
   if (!c) return;
   c->impl.destroy();
   delete c;
@@ -30,6 +31,7 @@ QDC_API size_t qdc_circuit_qubits(const qdc_circuit* c) { return c->impl.n; }
 
 QDC_API const char* qdc_circuit_set_state_from_vector(qdc_circuit* c, const qdc_complex* vec,
                                                       size_t len) {
+  qdc::DeviceGuard keep;  // every entry point leaves the caller's device current
   // QuantizedTensor::set_from_host + get_qubits_number (quantized_tensor.rs:44-52, 76-80);
   // a sharded circuit takes its slices of the full vector (the initial layout is identity)
   qdc::Circuit& k = c->impl;
@@ -64,6 +66,7 @@ QDC_API size_t qdc_circuit_grad_size(const qdc_circuit* c) { return c->impl.grad
 QDC_API const char* qdc_circuit_execute(qdc_circuit* c, int mode, const qdc_complex* cg,
                                         const size_t* cl, size_t nc, const qdc_complex* vg,
                                         const size_t* vl, size_t nv, qdc_complex* dens) {
+  qdc::DeviceGuard keep;
   qdc::Flat cf(cg, cl, nc), vf(vg, vl, nv);
   return c->impl.execute(mode, cf, vf, dens);
 }
@@ -72,17 +75,19 @@ QDC_API const char* qdc_circuit_backward(qdc_circuit* c, const qdc_complex* dg, 
                                          size_t nd, const qdc_complex* cg, const size_t* cl,
                                          size_t nc, const qdc_complex* vg, const size_t* vl,
                                          size_t nv, qdc_complex* grads) {
+  qdc::DeviceGuard keep;
   qdc::Flat df(dg, dl, nd), cf(cg, cl, nc), vf(vg, vl, nv);
   return c->impl.backward(df, cf, vf, grads);
 }
 
 QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
                                           qdc_complex* host, size_t len) {
+  qdc::DeviceGuard keep;
   qdc::Circuit& k = c->impl;
   if (shard < 0 || (size_t)shard >= k.sh.size()) return qdc::fail("no local shard %d", shard);
   if (len != ((size_t)1 << k.nl)) return qdc::fail("shard length mismatch");
   const qdc::Shard& s = k.sh[shard];
-  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
+  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd_live ? s.bwd : nullptr;
   if (!src) return qdc::fail("state %d is not allocated", which);
   QDC_TRY(k.sync_all());  // every shard's work, not only this shard's stream
   QDC_TRY(s.c().use());
@@ -95,12 +100,13 @@ QDC_API const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard,
 // of states too large for one host copy, e.g. the uncompute error of a 64 GiB state.
 QDC_API const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, size_t offset,
                                           qdc_complex* host, size_t len) {
+  qdc::DeviceGuard keep;
   qdc::Circuit& k = c->impl;
   if (shard < 0 || (size_t)shard >= k.sh.size()) return qdc::fail("no local shard %d", shard);
   const size_t size = (size_t)1 << k.nl;
   if (offset > size || len > size - offset) return qdc::fail("range out of the shard");
   const qdc::Shard& s = k.sh[shard];
-  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd;
+  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd_live ? s.bwd : nullptr;
   if (!src) return qdc::fail("state %d is not allocated", which);
   QDC_TRY(k.sync_all());
   QDC_TRY(s.c().use());
@@ -142,6 +148,39 @@ QDC_API const char* qdc_circuit_get_state(qdc_circuit* c, int which, qdc_complex
   return nullptr;
 }
 
+// The whole physical state (every shard, global shard index = the top g physical bits) on
+// every process: the local shards are copied, the others come from their processes by one RCCL
+// broadcast each, staged through the remap scratch buffer (a shard of device memory, so no
+// process needs the whole state on its GPU).  Collective over the circuit's communicator.
+QDC_API const char* qdc_circuit_gather_state(qdc_circuit* c, int which, qdc_complex* host,
+                                             size_t len) {
+  qdc::DeviceGuard keep;
+  qdc::Circuit& k = c->impl;
+  if (len != ((size_t)1 << k.n)) return qdc::fail("state length mismatch");
+  const size_t shard = (size_t)1 << k.nl;
+  if (!k.ex.comm) {  // every shard is local
+    if ((int)k.sh.size() != k.ex.world) return qdc::fail("shards of other processes need a communicator");
+    for (size_t s = 0; s < k.sh.size(); ++s)
+      QDC_TRY(qdc_circuit_get_shard(c, which, (int)s, host + s * shard, shard));
+    return nullptr;
+  }
+  const qdc::Shard& s = k.sh[0];
+  const qdc::cx* src = which == 0 ? s.state : which == 1 ? s.initial : s.bwd_live ? s.bwd : nullptr;
+  // every rank takes the same path (which is the same everywhere), so none waits alone
+  if (!src) return qdc::fail("state %d is not allocated", which);
+  if (!s.scratch) return qdc::fail("no staging buffer");
+  QDC_TRY(k.sync_all());
+  QDC_TRY(s.c().use());
+  const hipStream_t st = s.c().stream;
+  for (int r = 0; r < k.ex.world; ++r) {
+    QDC_NCCL(ncclBroadcast(src, s.scratch, shard * 2, qdc::Exchange::type(), r, k.ex.comm, st));
+    QDC_HIP(hipMemcpyAsync(host + (size_t)r * shard, s.scratch, shard * sizeof(qdc_complex),
+                           hipMemcpyDeviceToHost, st));
+    QDC_HIP(hipStreamSynchronize(st));
+  }
+  return nullptr;
+}
+
 QDC_API const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world,
                                        int* rank, int* local_shards) {
   const qdc::Circuit& k = c->impl;
@@ -157,7 +196,11 @@ QDC_API const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int
 struct qdc_comm {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  int device = 0;                 // the rank's GPU (current when the communicator was made)
+  hipStream_t stream = nullptr;   // host-value collectives (qdc_comm_allreduce)
+  double* dbuf = nullptr;         // their device staging, QDC_COMM_VALS doubles
 };
+constexpr int QDC_COMM_VALS = 64;
 
 QDC_API const char* qdc_comm_unique_id(unsigned char id[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
@@ -175,6 +218,10 @@ QDC_API const char* qdc_comm_init(qdc_comm** out, int rank, int world,
   qdc_comm* c = new qdc_comm();
   c->rank = rank;
   c->world = world;
+  if (hipGetDevice(&c->device) != hipSuccess) {
+    delete c;
+    return qdc::fail("qdc_comm_init: no current HIP device");
+  }
   const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
   if (r != ncclSuccess) {
     delete c;
@@ -186,8 +233,39 @@ QDC_API const char* qdc_comm_init(qdc_comm** out, int rank, int world,
 
 QDC_API void qdc_comm_free(qdc_comm* c) {
   if (!c) return;
+  qdc::DeviceGuard keep;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->dbuf) (void)hipFree(c->dbuf);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// Sum (op 0) or maximum (op 1) of `count` host doubles over the communicator's ranks, in place
+// on every rank; count 0 is a barrier.  Lets a one-process-per-GPU job time itself (bench.py's
+// barrier and max over ranks) over the circuit's own RCCL communicator, without a second
+// collective stack in the process.
+QDC_API const char* qdc_comm_allreduce(qdc_comm* c, double* vals, int count, int op) {
+  if (!c) return qdc::fail("no communicator");
+  if (count < 0 || count > QDC_COMM_VALS) return qdc::fail("allreduce of %d values (max %d)", count, QDC_COMM_VALS);
+  if (op != 0 && op != 1) return qdc::fail("allreduce op %d (0 sum, 1 max)", op);
+  if (c->world == 1) return nullptr;
+  qdc::DeviceGuard keep;
+  QDC_HIP(hipSetDevice(c->device));
+  if (!c->stream) QDC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  if (!c->dbuf) QDC_HIP(hipMalloc(&c->dbuf, sizeof(double) * QDC_COMM_VALS));
+  const int m = count > 0 ? count : 1;
+  if (count > 0)
+    QDC_HIP(hipMemcpyAsync(c->dbuf, vals, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+  else
+    QDC_HIP(hipMemsetAsync(c->dbuf, 0, sizeof(double), c->stream));
+  QDC_NCCL(ncclAllReduce(c->dbuf, c->dbuf, m, ncclDouble, op == 0 ? ncclSum : ncclMax, c->comm,
+                         c->stream));
+  if (count > 0)
+    QDC_HIP(hipMemcpyAsync(vals, c->dbuf, sizeof(double) * count, hipMemcpyDeviceToHost, c->stream));
+  QDC_HIP(hipStreamSynchronize(c->stream));
+  return nullptr;
 }
 
 static const char* new_circuit(qdc_circuit** out, size_t n, int world, int rank0, int nlocal,
@@ -240,19 +318,17 @@ QDC_API const char* qdc_circuit_new_devices(qdc_circuit** out, size_t n, int nde
     if (d < 0 || d >= count) return qdc::fail("device %d does not exist (%d visible)", d, count);
   QDC_TRY(qdc::check_n(n));
   const uint32_t g = qdc::log2_exact((size_t)ndev);
-  if (g == UINT32_MAX || (g > 0 && n < 2 * (size_t)g + 3))
-    return qdc::fail("%d devices cannot shard %zu qubits (a power of two, n >= 2g + 3)", ndev, n);
-  int cur = 0;
-  QDC_HIP(hipGetDevice(&cur));
+  if (g == UINT32_MAX || g > 8 || (g > 0 && n < 2 * (size_t)g + 3))
+    return qdc::fail("%d devices cannot shard %zu qubits (a power of two <= 256, n >= 2g + 3)",
+                     ndev, n);
+  qdc::DeviceGuard keep;
   std::vector<ncclComm_t> comms;
   if (ndev > 1 && distinct) {
     comms.resize(ndev);
     QDC_NCCL(ncclCommInitAll(comms.data(), ndev, devs.data()));
   }
   // from here the circuit owns the communicators (its destroy() frees them, also on error)
-  const char* e = new_circuit(out, n, ndev, 0, ndev, nullptr, &devs, &comms);
-  (void)hipSetDevice(cur);
-  return e;
+  return new_circuit(out, n, ndev, 0, ndev, nullptr, &devs, &comms);
 }
 
 // ---- planner -----------------------------------------------------------------------------
@@ -280,9 +356,13 @@ QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned
   return plan.size();
 }
 
-QDC_API const char* qdc_circuit_sync(qdc_circuit* c) { return c->impl.sync_all(); }
+QDC_API const char* qdc_circuit_sync(qdc_circuit* c) {
+  qdc::DeviceGuard keep;
+  return c->impl.sync_all();
+}
 
 QDC_API const char* qdc_circuit_profile(qdc_circuit* c, int on) {
+  qdc::DeviceGuard keep;
   for (auto& d : c->impl.devs) {
     qdc::Ctx& x = d->ctx;
     if (on) {

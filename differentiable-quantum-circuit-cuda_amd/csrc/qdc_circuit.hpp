@@ -85,6 +85,7 @@ struct Shard {
   cx* initial = nullptr;
   cx* state = nullptr;
   cx* bwd = nullptr;
+  bool bwd_live = false;  // bwd holds a cotangent (written by a backward): readable
   cx* scratch = nullptr;  // all-to-all staging (allocated when world > 1)
   std::vector<void*> owned;  // state allocations (remaps swap the pointers above among them)
   cx* dens = nullptr;
@@ -271,6 +272,9 @@ struct Circuit {
   const char* init(uint32_t qubits, int world = 1, int rank0 = 0, int nlocal = 1,
                    ncclComm_t comm = nullptr, const std::vector<int>* devices = nullptr,
                    const std::vector<ncclComm_t>* comms = nullptr) {
+    DeviceGuard keep;
+    // the communicators are owned from here on (destroy() frees them, also on a failure below)
+    if (comms) ex.comms = *comms;
     n = qubits;
     const uint32_t gg = log2_exact((size_t)world);
     if (gg == UINT32_MAX || gg > 8) return fail("the number of shards must be a power of two <= 256");
@@ -282,7 +286,6 @@ struct Circuit {
     ex.rank0 = rank0;
     ex.nlocal = nlocal;
     ex.comm = comm;
-    if (comms) ex.comms = *comms;
     ex.multi_stream = devices != nullptr && ex.comms.empty() && nlocal > 1;
     layout.identity(n, g);
     if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
@@ -335,10 +338,10 @@ struct Circuit {
       QDC_TRY(copy_initial(sh[s]));
     }
     QDC_TRY(sync_all());
-    QDC_HIP(hipSetDevice(cur));
     return nullptr;
   }
   void destroy() {
+    DeviceGuard keep;
     (void)sync_all();
     for (auto& s : sh) {
       if (s.d) (void)s.d->ctx.use();
@@ -375,8 +378,16 @@ struct Circuit {
     // block size: 2^12 chunks (QDC_STATE_ILV_BITS); states of at least two blocks
     uint32_t gb = 12;
     if (const char* b = getenv("QDC_STATE_ILV_BITS")) gb = (uint32_t)std::max(4, std::min(atoi(b), 24));
-    const bool ilv = !(e && atoi(e) == 0) && g == 0 && sh.size() == 1 &&
-                     nchunks_of(nl) >= ((uint64_t)2 << gb);
+    bool ilv = !(e && atoi(e) == 0) && g == 0 && sh.size() == 1 &&
+               nchunks_of(nl) >= ((uint64_t)2 << gb);
+    if (ilv) {
+      // the pair allocates bwd now, not on the first backward (circuit.rs:276 creates it
+      // lazily): when the device cannot hold it beside `initial` plus 1 GiB of headroom, keep
+      // the plain layout, so a run/forward-only circuit still needs only two states
+      size_t free_b = 0, total_b = 0;
+      QDC_HIP(hipMemGetInfo(&free_b, &total_b));
+      if (free_b < 2 * bytes + ((size_t)1 << 30)) ilv = false;
+    }
     if (ilv) {
       gap_bits = gb;
       gm = ~(((uint64_t)1 << gap_bits) - 1);
@@ -1328,12 +1339,14 @@ struct Circuit {
     std::vector<size_t> gidx;
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
     const size_t nvar = n_var();
-    for (auto& s : sh)
+    for (auto& s : sh) {
       if (!s.bwd) {
         QDC_TRY(s.c().use());
         QDC_HIP(hipMalloc(&s.bwd, ((size_t)1 << nl) * sizeof(cx)));
         s.owned.push_back(s.bwd);
       }
+      s.bwd_live = true;
+    }
     // slots [0, nvar): per-gate gradients; [nvar, nvar + stages): fused stages' Gamma
     const size_t nslots = std::max<size_t>(2 * nvar, 1);
     QDC_TRY(ensure_out(false, nslots * RED));

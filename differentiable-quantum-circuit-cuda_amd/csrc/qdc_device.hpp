@@ -92,6 +92,22 @@ struct Prof {
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t NBMAX = 4096;  // max blocks of a reduction launch = partials per slot
 
+// Restores the caller's current HIP device on every return path of a C-ABI entry point: a
+// multi-device circuit switches devices per shard (Ctx::use), and the primitives, torch and
+// the caller's own code must not find themselves on the last shard's GPU afterwards.
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (dev >= 0 && (hipGetDevice(&cur) != hipSuccess || cur != dev)) (void)hipSetDevice(dev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -169,6 +185,7 @@ struct Ctx {
     return nullptr;
   }
   void destroy() {
+    DeviceGuard keep;
     if (stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);

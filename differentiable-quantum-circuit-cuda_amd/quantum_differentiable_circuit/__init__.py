@@ -213,22 +213,18 @@ class _CircuitBase:
 
     def get_state(self, which: int = 0) -> np.ndarray:
         """Copy of the forward (0), initial (1) or backward (2) state in logical qubit order.
-        Sharded over processes: the local shards are gathered with torch.distributed."""
+        Sharded over processes: collective — the shards are gathered over the circuit's own
+        RCCL communicator (qdc_circuit_gather_state)."""
         phys, world, rank0, nlocal = self.layout()
+        out = np.empty(1 << self._n, dtype=self._dtype)
         if world == 1:
-            out = np.empty(1 << self._n, dtype=self._dtype)
             # (logical order: the library undoes a permuted single-device layout)
             check(self._lib.qdc_circuit_get_state(self._h, which, ptr(out), out.size))
             return out
-        shards = [self.get_shard(which, s) for s in range(nlocal)]
-        if nlocal < world:
-            import torch.distributed as dist  # plumbing only
-            got = [None] * world
-            dist.all_gather_object(got, shards[0])
-            shards = got
+        check(self._lib.qdc_circuit_gather_state(self._h, which, ptr(out), out.size))
         if which == 1:
             phys = list(range(self._n))  # `initial` is always in the identity layout
-        return unpermute(np.concatenate(shards), phys)
+        return unpermute(out, phys)
 
     def synchronize(self):
         check(self._lib.qdc_circuit_sync(self._h))

@@ -31,7 +31,7 @@ RUNTIME = (
     "qdc_circuit_output_size", "qdc_circuit_grad_size", "qdc_circuit_execute",
     "qdc_circuit_backward", "qdc_circuit_get_state", "qdc_circuit_sync", "qdc_circuit_profile",
     "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
-    "qdc_comm_free", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
+    "qdc_comm_free", "qdc_comm_allreduce", "qdc_circuit_gather_state", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
     "qdc_circuit_new_devices",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
     "qdc_rq_plan", "qdc_gate_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
@@ -97,6 +97,8 @@ def _proto(lib):
         "qdc_comm_unique_id": (_E, [C.c_char_p]),
         "qdc_comm_init": (_E, [C.POINTER(_P), C.c_int, C.c_int, C.c_char_p]),
         "qdc_comm_free": (None, [_P]),
+        "qdc_comm_allreduce": (_E, [_P, C.POINTER(C.c_double), C.c_int, C.c_int]),
+        "qdc_circuit_gather_state": (_E, [_P, C.c_int, _P, _S]),
         "qdc_circuit_new_sharded": (_E, [C.POINTER(_P), _S, _P]),
         "qdc_circuit_new_local_shards": (_E, [C.POINTER(_P), _S, C.c_int]),
         "qdc_circuit_new_devices": (_E, [C.POINTER(_P), _S, C.c_int, C.POINTER(C.c_int)]),

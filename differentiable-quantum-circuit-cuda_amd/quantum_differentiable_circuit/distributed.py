@@ -2,12 +2,16 @@
 
 The native runtime owns the RCCL communicator (C ABI qdc_comm_*).  Rank 0 creates the
 128-byte ncclUniqueId and publishes it in a file (written to a temporary name, then renamed, so
-a reader never sees a partial id); the other ranks poll for it.  The file name is unique per
-launch (QDC_NCCL_ID_FILE, else derived from MASTER_ADDR/MASTER_PORT and the run id that
-torchrun or any launcher exports); rank 0 removes it once the communicator exists
-(ncclCommInitRank returns only after every rank has joined, i.e. has read it).  Usage, under
-any launcher that exports RANK / WORLD_SIZE / LOCAL_RANK (torchrun, mpirun wrappers, a shell
-loop):
+a reader never sees a partial id); the other ranks poll for it.  The file is bound to this
+launch twice over: its name carries MASTER_ADDR/MASTER_PORT, the launcher's run id and the
+launcher's process id (the ranks' common parent under torchrun or mpirun), and its contents
+carry rank 0's start time, which a reader accepts only within `skew` seconds of its own start
+— so an id left behind by an earlier launch that died before rank 0 removed it (same name:
+a shell loop relaunching from one parent) is never taken for this launch's.  rank 0 removes it
+once the communicator exists (ncclCommInitRank returns only after every rank has joined, i.e.
+has read it).  The file lives in the node's temporary directory: this bootstrap is single-node
+(QDC_NCCL_ID_FILE may name a shared path for more).  Usage, under any launcher that exports
+RANK / WORLD_SIZE / LOCAL_RANK (torchrun, mpirun wrappers, a shell loop):
 
     from quantum_differentiable_circuit import circuit_class
     from quantum_differentiable_circuit.distributed import Communicator
@@ -20,6 +24,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import struct
 import tempfile
 import time
 from pathlib import Path
@@ -40,29 +45,50 @@ def default_id_file(world: int) -> Path:
     tag = "_".join(os.environ.get(k, "x") for k in ("MASTER_ADDR", "MASTER_PORT",
                                                      "TORCHELASTIC_RUN_ID"))
     tag = "".join(ch if ch.isalnum() else "_" for ch in tag)
-    return Path(tempfile.gettempdir()) / f"qdc_nccl_id_{tag}_w{world}"
+    return Path(tempfile.gettempdir()) / f"qdc_nccl_id_{tag}_p{os.getppid()}_w{world}"
 
 
-def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0) -> bytes:
-    """Rank 0 publishes make_id()'s 128 bytes at `path` (temporary name + rename: never seen
-    partial); every other rank polls for it."""
+def process_start_time() -> float:
+    """Wall-clock start of this process (Linux /proc; else now)."""
+    try:
+        ticks = int(Path("/proc/self/stat").read_text().rsplit(")", 1)[1].split()[19])
+        boot = next(float(l.split()[1]) for l in Path("/proc/stat").read_text().splitlines()
+                    if l.startswith("btime"))
+        return boot + ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError, StopIteration):
+        return time.time()
+
+
+_ID_LEN = 128
+_FMT = "<d"  # rank 0's start time after the id
+
+
+def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: float = 120.0,
+                start: float | None = None) -> bytes:
+    """Rank 0 publishes make_id()'s 128 bytes and its start time at `path` (temporary name +
+    rename: never seen partial); every other rank polls for a file whose rank-0 start time is
+    within `skew` s of its own start (ranks of one launch start together; a stale file of an
+    earlier launch is older)."""
     path = Path(path)
+    start = process_start_time() if start is None else start
     if rank == 0:
         raw = make_id()
         tmp = path.with_name(path.name + f".tmp{os.getpid()}")
-        tmp.write_bytes(raw)
+        tmp.write_bytes(raw + struct.pack(_FMT, start))
         os.replace(tmp, path)
         return raw
     t0 = time.monotonic()
     while True:
         try:
-            raw = path.read_bytes()
-            if len(raw) == 128:
-                return raw
+            data = path.read_bytes()
+            if len(data) == _ID_LEN + struct.calcsize(_FMT):
+                (t_root,) = struct.unpack(_FMT, data[_ID_LEN:])
+                if abs(t_root - start) <= skew:
+                    return data[:_ID_LEN]
         except FileNotFoundError:
             pass
         if time.monotonic() - t0 > timeout:
-            raise TimeoutError(f"rank {rank}: no RCCL id at {path} after {timeout} s")
+            raise TimeoutError(f"rank {rank}: no RCCL id of this launch at {path} after {timeout} s")
         time.sleep(0.05)
 
 
@@ -93,6 +119,22 @@ class Communicator:
                 path.unlink()
             except FileNotFoundError:
                 pass
+
+    # host-value collectives over the same RCCL communicator (qdc_comm_allreduce)
+    def allreduce(self, values, op: str = "sum"):
+        vals = [float(v) for v in values]
+        arr = (C.c_double * max(len(vals), 1))(*vals)
+        check(self._lib.qdc_comm_allreduce(self.handle, arr, len(vals), 0 if op == "sum" else 1))
+        return [arr[i] for i in range(len(vals))]
+
+    def barrier(self):
+        check(self._lib.qdc_comm_allreduce(self.handle, None, 0, 0))
+
+    def max(self, x: float) -> float:
+        return self.allreduce([x], "max")[0]
+
+    def sum(self, x: float) -> float:
+        return self.allreduce([x], "sum")[0]
 
     def __del__(self):
         h = getattr(self, "handle", None)

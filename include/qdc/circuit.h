@@ -126,11 +126,15 @@ const char* qdc_build_info(void);
  *   - qdc_circuit_new_local_shards: every shard on the current GPU, exchanged with device
  *     copies (the same data path on one GPU; used by the single-GPU parity tests). */
 typedef struct qdc_comm qdc_comm;
-/* rank 0 creates the id and ships it to the other ranks (e.g. torch.distributed broadcast) */
+/* rank 0 creates the id and ships it to the other ranks (quantum_differentiable_circuit.
+ * distributed: through a per-launch file, no second collective stack) */
 const char* qdc_comm_unique_id(unsigned char id[128]);
 /* collective over all ranks; uses the current HIP device */
 const char* qdc_comm_init(qdc_comm** out, int rank, int world, const unsigned char id[128]);
 void qdc_comm_free(qdc_comm* comm);
+/* Collective: sum (op 0) or maximum (op 1) of `count` <= 64 host doubles over the ranks, in
+ * place on every rank; count 0 is a barrier.  Returns after the result is on the host. */
+const char* qdc_comm_allreduce(qdc_comm* comm, double* vals, int count, int op);
 
 const char* qdc_circuit_new_sharded(qdc_circuit** out, size_t qubits_number, qdc_comm* comm);
 const char* qdc_circuit_new_local_shards(qdc_circuit** out, size_t qubits_number, int shards);
@@ -148,6 +152,11 @@ const char* qdc_circuit_layout(const qdc_circuit* c, unsigned* phys, int* world,
 /* Copy of one local shard (2^(n-g) amplitudes, physical order). which: 0 fwd, 1 initial, 2 bwd */
 const char* qdc_circuit_get_shard(qdc_circuit* c, int which, int shard, qdc_complex* host,
                                   size_t len);
+
+/* Collective over the circuit's communicator: the whole state (2^n amplitudes, PHYSICAL
+ * order: shard r = physical index bits above n - g equal to r) on every process, shards of
+ * other processes broadcast through one shard of device staging.  which: as qdc_circuit_get_shard */
+const char* qdc_circuit_gather_state(qdc_circuit* c, int which, qdc_complex* host, size_t len);
 
 /* A range [offset, offset + len) of one local shard in PHYSICAL order (qubits may be permuted:
  * qdc_circuit_layout); for streaming reads of states too large for one host copy. */

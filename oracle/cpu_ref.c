@@ -8,8 +8,9 @@
  *   INSERT_ZERO(mask, off) = ((mask & off) << 1) | (~mask & off)      primitives.cu:104-105
  *   two-qubit kernels insert the zero at the lower position first      primitives.cu:305-321
  * but with 64-bit sizes (the reference's `1 << n` is an int, primitives.cu:147).
- * Reductions accumulate `+=` into the caller's buffer like the host loops of
- * primitives.cu:281-288.  Arithmetic is sequential per element: out[p] = sum_q g[2p+q] in[q].
+ * Reductions follow the reference's 128 x 128-thread summation order and accumulate `+=` into
+ * the caller's buffer like the host loops of primitives.cu:281-288.  Arithmetic is sequential
+ * per element: out[p] = sum_q g[2p+q] in[q].
  *
  * Build: gcc -O3 -fopenmp -shared -fPIC [-DQDC_F64]  (oracle/Makefile)
  */
@@ -95,32 +96,52 @@ EXPORT void cref_q2gate_diag(C* s, const C* d, size_t pos2, size_t pos1, size_t 
   }
 }
 
-/* Reductions: per-thread partials, summed in thread order, then `+=` (primitives.cu:281-288). */
-#define REDUCE_BEGIN(K)                        \
-  C acc_total[K];                              \
-  for (int k_ = 0; k_ < K; ++k_) acc_total[k_] = 0; \
-  _Pragma("omp parallel")                      \
-  {                                            \
-    C acc[K];                                  \
-    for (int k_ = 0; k_ < K; ++k_) acc[k_] = 0;
-#define REDUCE_END(K, out)                                   \
-    _Pragma("omp critical")                                  \
-    for (int k_ = 0; k_ < K; ++k_) acc_total[k_] += acc[k_]; \
-  }                                                          \
-  for (int k_ = 0; k_ < K; ++k_) out[k_] += acc_total[k_];
+/* Reductions, in the reference's summation order (primitives.cu:202-292 and its siblings):
+ * BLOCKS_NUM x THREADS_NUM = 128 x 128 CUDA threads (pr.cu:6-7); thread v accumulates the items
+ * tid = v, v + 16384, v + 2 * 16384, ... sequentially (PARALLEL_FOR, pr.cu:72-80); each block
+ * folds its 128 partials by the shared-memory tree s = 64, 32, ..., 1 (cache[t] += cache[t + s]);
+ * the host then adds the 128 block sums in block order into the caller's buffer with `+=`
+ * (pr.cu:281-288).  So the f32 rounding of a long reduction is the reference's, not that of one
+ * long sequential sum per OpenMP thread (which at n = 24 is ~1e-4 in f32, 100x the reference's).
+ * Items are visited row by row (row r = items r * 16384 .. + 16383) so memory streams in order;
+ * an OpenMP thread owns a range of virtual threads and their K accumulators. */
+#define REF_BLOCKS 128
+#define REF_THREADS 128
+#define REF_VT (REF_BLOCKS * REF_THREADS)
+#define REDUCE_BEGIN(K, BATCH)                                                   \
+  enum { K_ = (K) };                                                             \
+  const int64_t batch_ = (int64_t)(BATCH);                                       \
+  C* part_ = (C*)calloc((size_t)REF_VT * K_, sizeof(C));                         \
+  if (!part_) abort();                                                           \
+  _Pragma("omp parallel")                                                        \
+  {                                                                              \
+    const int nt_ = omp_get_num_threads(), me_ = omp_get_thread_num();           \
+    const int64_t v0_ = (int64_t)REF_VT * me_ / nt_, v1_ = (int64_t)REF_VT * (me_ + 1) / nt_; \
+    for (int64_t r0_ = 0; r0_ < batch_; r0_ += REF_VT)                           \
+      for (int64_t v_ = v0_; v_ < v1_ && r0_ + v_ < batch_; ++v_) {              \
+        const int64_t tid = r0_ + v_;                                            \
+        C* acc = part_ + (size_t)v_ * K_;
+#define REDUCE_END(out)                                                          \
+      }                                                                          \
+  }                                                                              \
+  for (int b_ = 0; b_ < REF_BLOCKS; ++b_) {                                      \
+    C* blk_ = part_ + (size_t)b_ * REF_THREADS * K_;                             \
+    for (int s_ = REF_THREADS / 2; s_ != 0; s_ /= 2)                             \
+      for (int t_ = 0; t_ < s_; ++t_)                                            \
+        for (int k_ = 0; k_ < K_; ++k_) blk_[t_ * K_ + k_] += blk_[(t_ + s_) * K_ + k_]; \
+  }                                                                              \
+  for (int b_ = 0; b_ < REF_BLOCKS; ++b_)                                        \
+    for (int k_ = 0; k_ < K_; ++k_) (out)[k_] += part_[(size_t)b_ * REF_THREADS * K_ + k_]; \
+  free(part_);
 
 /* primitives.cu:689-739 */
 EXPORT void cref_q1density(const C* s, C* rho, size_t pos, size_t n) {
   const uint64_t mask = UINT64_MAX << pos, stride = (uint64_t)1 << pos;
-  const int64_t batch = (int64_t)(((uint64_t)1 << n) >> 1);
-  REDUCE_BEGIN(4)
-#pragma omp for schedule(static)
-  for (int64_t tid = 0; tid < batch; ++tid) {
+  REDUCE_BEGIN(4, ((uint64_t)1 << n) >> 1)
     const uint64_t b = insert_zero(mask, (uint64_t)tid);
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 2; ++p) acc[2 * p + q] += s[p * stride + b] * CONJ(s[q * stride + b]);
-  }
-  REDUCE_END(4, rho)
+  REDUCE_END(rho)
 }
 
 /* primitives.cu:779-837 */
@@ -128,32 +149,24 @@ EXPORT void cref_q2density(const C* s, C* rho, size_t pos2, size_t pos1, size_t 
   uint64_t mn, mx;
   q2_masks(pos2, pos1, &mn, &mx);
   const uint64_t s1 = (uint64_t)1 << pos1, s2 = (uint64_t)1 << pos2;
-  const int64_t batch = (int64_t)(((uint64_t)1 << n) >> 2);
-  REDUCE_BEGIN(16)
-#pragma omp for schedule(static)
-  for (int64_t tid = 0; tid < batch; ++tid) {
+  REDUCE_BEGIN(16, ((uint64_t)1 << n) >> 2)
     const uint64_t b = insert_zero(mx, insert_zero(mn, (uint64_t)tid));
     C x[4];
     for (int p2 = 0; p2 < 2; ++p2)
       for (int p1 = 0; p1 < 2; ++p1) x[2 * p2 + p1] = s[b + p2 * s2 + p1 * s1];
     for (int p = 0; p < 4; ++p)
       for (int q = 0; q < 4; ++q) acc[4 * p + q] += x[p] * CONJ(x[q]);
-  }
-  REDUCE_END(16, rho)
+  REDUCE_END(rho)
 }
 
 /* primitives.cu:202-253 */
 EXPORT void cref_q1grad(const C* f, const C* bw, C* grad, size_t pos, size_t n) {
   const uint64_t mask = UINT64_MAX << pos, stride = (uint64_t)1 << pos;
-  const int64_t batch = (int64_t)(((uint64_t)1 << n) >> 1);
-  REDUCE_BEGIN(4)
-#pragma omp for schedule(static)
-  for (int64_t tid = 0; tid < batch; ++tid) {
+  REDUCE_BEGIN(4, ((uint64_t)1 << n) >> 1)
     const uint64_t b = insert_zero(mask, (uint64_t)tid);
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 2; ++p) acc[2 * p + q] += bw[p * stride + b] * f[q * stride + b];
-  }
-  REDUCE_END(4, grad)
+  REDUCE_END(grad)
 }
 
 /* primitives.cu:295-354 */
@@ -161,10 +174,7 @@ EXPORT void cref_q2grad(const C* f, const C* bw, C* grad, size_t pos2, size_t po
   uint64_t mn, mx;
   q2_masks(pos2, pos1, &mn, &mx);
   const uint64_t s1 = (uint64_t)1 << pos1, s2 = (uint64_t)1 << pos2;
-  const int64_t batch = (int64_t)(((uint64_t)1 << n) >> 2);
-  REDUCE_BEGIN(16)
-#pragma omp for schedule(static)
-  for (int64_t tid = 0; tid < batch; ++tid) {
+  REDUCE_BEGIN(16, ((uint64_t)1 << n) >> 2)
     const uint64_t b = insert_zero(mx, insert_zero(mn, (uint64_t)tid));
     C xf[4], xb[4];
     for (int p2 = 0; p2 < 2; ++p2)
@@ -174,8 +184,7 @@ EXPORT void cref_q2grad(const C* f, const C* bw, C* grad, size_t pos2, size_t po
       }
     for (int p = 0; p < 4; ++p)
       for (int q = 0; q < 4; ++q) acc[4 * p + q] += xb[p] * xf[q];
-  }
-  REDUCE_END(16, grad)
+  REDUCE_END(grad)
 }
 
 /* primitives.cu:398-452 */
@@ -184,16 +193,12 @@ EXPORT void cref_q2grad_diag(const C* f, const C* bw, C* grad, size_t pos2, size
   uint64_t mn, mx;
   q2_masks(pos2, pos1, &mn, &mx);
   const uint64_t s1 = (uint64_t)1 << pos1, s2 = (uint64_t)1 << pos2;
-  const int64_t batch = (int64_t)(((uint64_t)1 << n) >> 2);
-  REDUCE_BEGIN(4)
-#pragma omp for schedule(static)
-  for (int64_t tid = 0; tid < batch; ++tid) {
+  REDUCE_BEGIN(4, ((uint64_t)1 << n) >> 2)
     const uint64_t b = insert_zero(mx, insert_zero(mn, (uint64_t)tid));
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 2; ++p)
         acc[2 * p + q] += bw[p * s2 + q * s1 + b] * f[p * s2 + q * s1 + b];
-  }
-  REDUCE_END(4, grad)
+  REDUCE_END(grad)
 }
 
 /* primitives.cu:176-187 */

@@ -156,6 +156,27 @@ def test_layered_c2_parity(prec):
     fl.check("uncomputed", c.get_state(0), f"C2 n={n} {prec} ")
 
 
+@pytest.mark.timeout(900)
+def test_layered_c2_n24_f32_vs_f64_restatement():
+    """BASELINE config 2 at its stated size: C2's generator at n = 24, f32, forward + backward
+    on the GPU, against the reference algorithm in complex128 (the C restatement of its kernels,
+    CRefOps("f64"), driven in circuit.rs order — exact to ~1e-15 here, far below the f32
+    floor).  The floor is the same restatement in f32.  4 layers (220 gates, 24 densities): the
+    two host runs of the reference algorithm take about a minute on the box's cores."""
+    import quantum_differentiable_circuit as q
+    from oracle.cref import CRefOps
+    n = 24
+    ins, var = O.layered_circuit(n, layers=4, seed=24)
+    fl = F.Floor("f32", n, ins, [], var, run=False, exact_ops=CRefOps("f64"))
+    c = q.circuit_class("f32")(n)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    fl.check("forward", c.forward([], fl.var), f"C2 n={n} f32 ")
+    fl.check("grads", c.backward(fl.cots, [], fl.var), f"C2 n={n} f32 ")
+    fl.check("uncomputed", c.get_state(0), f"C2 n={n} f32 ")
+    fl.check("bwd", c.get_state(2), f"C2 n={n} f32 ")
+
+
 def test_uncompute_roundtrip_large():
     """Size-independent property at a large size (n = 26, f32): the O(1)-memory reverse sweep
     returns the forward state to the initial state, and gradients of unitary circuits satisfy

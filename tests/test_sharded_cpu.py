@@ -276,3 +276,27 @@ def test_rccl_id_file_exchange(tmp_path):
     for p in ps:
         p.join(timeout=60)
     assert all(v == bytes(range(128)) for v in got.values()) and len(got) == 4
+
+
+def test_rccl_id_file_rejects_stale(tmp_path):
+    """An id file left by an earlier launch (rank 0 died before removing it) carries that
+    launch's rank-0 start time: a reader of this launch keeps polling instead of taking it, and
+    takes the fresh file once this launch's rank 0 writes it."""
+    import struct
+    import threading
+    from quantum_differentiable_circuit.distributed import exchange_id
+    path = tmp_path / "nccl.id"
+    now = 1.0e9
+    path.write_bytes(bytes([7] * 128) + struct.pack("<d", now - 3600.0))  # stale, an hour old
+    got = {}
+
+    def reader():
+        got["raw"] = exchange_id(1, path, None, timeout=30, start=now + 1.0)
+
+    t = threading.Thread(target=reader)
+    t.start()
+    t.join(timeout=0.5)
+    assert t.is_alive() and "raw" not in got  # still polling: the stale id was rejected
+    exchange_id(0, path, lambda: bytes(range(128)), start=now)
+    t.join(timeout=30)
+    assert got["raw"] == bytes(range(128))
