@@ -248,6 +248,7 @@ struct Circuit {
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
   uint32_t last_fused_grid = 0;
+  uint32_t last_fused_ndyn = 0;  // granule partials per slot of the last fused launch
   unsigned char* prog_host = nullptr;  // pinned staging of the pass program (every device's copy)
   std::vector<StagePost> stage_post;   // gradient recipes of the last backward's stages
   size_t prog_cap = 0;
@@ -1028,6 +1029,7 @@ struct Circuit {
     grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
+    last_fused_ndyn = 0;
     return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, NT>(), grid, (uint32_t)NT,
                             f, b, fops, mats, g, partials, stride);
   }
@@ -1052,12 +1054,16 @@ struct Circuit {
       uint32_t grid = 0;
       QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
       fgeo g = fg;
-      uint64_t tpb = 1;
-      while (tpb * grid < g.ntiles) tpb <<= 1;
-      g.tpb = (uint32_t)tpb;
-      grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+      // one wave per block: static shares + a dynamic tail
+      if (!(bs == 64 && !pfw && grid >= 8 && g.ntiles >= 4ull * grid && ctx.plan_dyn(g, grid))) {
+        uint64_t tpb = 1;
+        while (tpb * grid < g.ntiles) tpb <<= 1;
+        g.tpb = (uint32_t)tpb;
+        grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+      }
       if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
       last_fused_grid = grid;
+      last_fused_ndyn = g.ndyn ? ctx.last_ndyn : 0u;
       if (two && pfw)
         return ctx.launch_block(name, bytes, k_rw<true, 2, true, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
@@ -1093,6 +1099,7 @@ struct Circuit {
     grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
+    last_fused_ndyn = 0;
 #define QDC_RQ_LAUNCH(T, N, P)                                                            \
   if (two == T && nt == N && pf == P)                                                     \
     return ctx.launch_block(name, bytes, k_rq<T, N, P>, grid, nt, f, b, fops, mats, g, l0, \
@@ -1120,12 +1127,16 @@ struct Circuit {
     uint32_t grid = 0;
     QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
     fgeo g = fg;
-    uint64_t tpb = 1;
-    while (tpb * grid < g.ntiles) tpb <<= 1;
-    g.tpb = (uint32_t)tpb;
-    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    // one wave per block: static shares + a dynamic tail
+    if (!(bs == 64 && grid >= 8 && g.ntiles >= 4ull * grid && ctx.plan_dyn(g, grid))) {
+      uint64_t tpb = 1;
+      while (tpb * grid < g.ntiles) tpb <<= 1;
+      g.tpb = (uint32_t)tpb;
+      grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    }
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
+    last_fused_ndyn = g.ndyn ? ctx.last_ndyn : 0u;
     if (two)
       return ctx.launch_block(name, bytes, k_rw<true, 1, false, 1>, grid, bs, f, b, fops, mats, g, l0,
                               partials, stride);
@@ -1211,7 +1222,7 @@ struct Circuit {
         QDC_TRY((launch_fused<false, true, false>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       }
       if (fg.ngrad > 0)
-        for (uint32_t slot : it.grad_slots) ctx.commit(slot, last_fused_grid);
+        for (uint32_t slot : it.grad_slots) ctx.commit(slot, last_fused_grid, last_fused_ndyn);
     }
     // a permuting pass stored its tile's qubits at new positions (later ops were planned so)
     for (const auto& sw : it.swaps) layout.swap_phys(sw.first, sw.second);
@@ -1248,9 +1259,17 @@ struct Circuit {
     return apply_dense<4>(ctx, s, a, p2, p1, nl, uncompute ? "uncompute_q2" : "apply_q2");
   }
 
+  const char* dyn_reset_all() {
+    for (auto& d : devs) {
+      QDC_TRY(d->ctx.use());
+      QDC_TRY(d->ctx.dyn_reset());
+    }
+    return nullptr;
+  }
   const char* execute(int mode, const Flat& cg, const Flat& vg, qdc_complex* out) {
     std::vector<size_t> gidx;
     QDC_TRY(validate_forward(cg, vg, gidx));
+    QDC_TRY(dyn_reset_all());
     const size_t nout = output_count(mode);
     QDC_TRY(ensure_out(true, std::max<size_t>(nout, 1) * RED));
     // every pass starts from `initial`, which is always in the identity layout
@@ -1338,6 +1357,7 @@ struct Circuit {
   const char* backward(const Flat& dg, const Flat& cg, const Flat& vg, qdc_complex* out) {
     std::vector<size_t> gidx;
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
+    QDC_TRY(dyn_reset_all());
     const size_t nvar = n_var();
     for (auto& s : sh) {
       if (!s.bwd) {

@@ -151,6 +151,15 @@ struct Ctx {
   cx* pending_base = nullptr;
   int pending_accumulate = 0;
   Prof prof;
+  unsigned long long* dctr = nullptr;  // 8 dynamic-tail counters (plan_dyn)
+  uint64_t dbase = 0;
+  uint32_t dyn_static_pct = 35;  // QDC_DYN: static share of the fair share, % (100: off)
+  // granule partials of dynamic-tail passes: [FIN_MAX][DYN_CAP][RED], slot i beside partials'
+  cx* dparts = nullptr;
+  cx* dsums = nullptr;  // [FIN_MAX][DYN_CAP / BLOCK][RED]: k_dsum's chunk sums
+  static constexpr uint32_t DYN_CAP = 65536;  // 256 MiB of granule partials, allocated on first use
+  std::vector<uint32_t> pending_nd;
+  uint32_t last_ndyn = 0;  // granules of the last launch planned by plan_dyn (0: static)
 
   const char* init(int dev) {
     device = dev;
@@ -159,6 +168,9 @@ struct Ctx {
     QDC_HIP(hipMalloc(&partials, sizeof(cx) * (size_t)FIN_MAX * NBMAX * RED));
     QDC_HIP(hipMalloc(&results, sizeof(cx) * (size_t)FIN_MAX * RED));
     QDC_HIP(hipHostMalloc(&host_results, sizeof(cx) * (size_t)FIN_MAX * RED));
+    QDC_HIP(hipMalloc(&dctr, sizeof(unsigned long long) * 8 * FG_DCTR_STRIDE));
+    QDC_TRY(dyn_reset());
+    if (const char* e = getenv("QDC_DYN")) dyn_static_pct = (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
@@ -178,6 +190,66 @@ struct Ctx {
     if (cur != device) QDC_HIP(hipSetDevice(device));
     return nullptr;
   }
+  // Dynamic-tail tile counters of the one-wave register-resident passes (fgeo::dctr): host
+  // and device agree on their value at each launch's start (dbase); re-zeroed at the start of
+  // every circuit call, so a failed launch can never leave them out of step for the next call.
+  const char* dyn_reset() {
+    if (!dctr) return nullptr;
+    QDC_HIP(hipMemsetAsync(dctr, 0, sizeof(unsigned long long) * 8 * FG_DCTR_STRIDE, stream));
+    dbase = 0;
+    return nullptr;
+  }
+  // static shares + dynamic tail of a launch of `grid` one-wave blocks over g.ntiles tiles:
+  // every block runs dyn_static_pct % of its fair share block-contiguously (g.tpb tiles), the
+  // rest is handed out by the eight pool counters; the counters then advance by ndyn / 8
+  // successful grabs + grid / 8 final empty ones each, alike, which dbase follows
+  // (false: no dynamic tail for this launch, g unchanged)
+  // (false: no dynamic tail for this launch, g unchanged).  Granules of dgran tiles keep the
+  // granule partials of a reducing pass within DYN_CAP per slot.
+  bool plan_dyn(fgeo& g, uint32_t grid) {
+    last_ndyn = 0;
+    if (!dctr || dyn_static_pct >= 100 || (grid & 7u) || (g.ntiles & 7u) || g.order == 1)
+      return false;
+    if (g.ngrad > 0 && !dparts) {  // first reducing dynamic pass of this context
+      if (hipMalloc(&dparts, sizeof(cx) * (size_t)FIN_MAX * DYN_CAP * RED) != hipSuccess ||
+          hipMalloc(&dsums, sizeof(cx) * (size_t)FIN_MAX * (DYN_CAP / BLOCK) * RED) != hipSuccess) {
+        (void)hipGetLastError();
+        if (dparts) (void)hipFree(dparts);
+        dparts = nullptr;
+        dyn_static_pct = 100;  // no room: static shares only from now on
+        return false;
+      }
+    }
+    uint64_t per = g.ntiles * dyn_static_pct / 100 / grid;
+    uint64_t ndyn = g.ntiles - per * grid;  // a multiple of 8 (ntiles and grid are)
+    uint32_t gran = 1;
+    if (g.ngrad > 0)
+      while (ndyn / gran > DYN_CAP || (ndyn % (8ull * gran)) != 0) {
+        if (gran >= 64) return false;
+        gran *= 2;
+        // whole granules: move the remainder of ndyn back into the static shares
+        const uint64_t rem = ndyn % (8ull * gran);
+        if (rem) {
+          const uint64_t add = (rem + grid - 1) / grid;  // more static tiles per block
+          per += add;
+          if (per * grid > g.ntiles) return false;
+          ndyn = g.ntiles - per * grid;
+          gran = 1;  // re-check from the smallest granule with the new split
+        }
+      }
+    if (ndyn == 0) return false;
+    g.tpb = (uint32_t)per;
+    g.nstat = per * grid;
+    g.ndyn = ndyn;
+    g.dgran = gran;
+    g.dctr = dctr;
+    g.dbase = dbase;
+    g.dpart = dparts + pending_dst.size() * (size_t)DYN_CAP * RED;
+    g.dstride = (uint64_t)DYN_CAP * RED;
+    dbase += ndyn / gran / 8 + grid / 8;
+    last_ndyn = g.ngrad > 0 ? (uint32_t)(ndyn / gran) : 0u;
+    return true;
+  }
   const char* sync() const {
     if (!stream) return nullptr;
     QDC_TRY(use());
@@ -193,6 +265,11 @@ struct Ctx {
     if (partials) (void)hipFree(partials);
     if (results) (void)hipFree(results);
     if (host_results) (void)hipHostFree(host_results);
+    if (dctr) (void)hipFree(dctr);
+    dctr = nullptr;
+    if (dparts) (void)hipFree(dparts);
+    if (dsums) (void)hipFree(dsums);
+    dparts = dsums = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     partials = results = host_results = nullptr;
     stream = nullptr;
@@ -235,9 +312,11 @@ struct Ctx {
     return nullptr;
   }
   cx* slot_ptr() const { return partials + pending_dst.size() * (size_t)NBMAX * RED; }
-  void commit(uint32_t dst, uint32_t nb) {
+  // nd: granule partials of a dynamic-tail pass in the slot's dparts row (0: none)
+  void commit(uint32_t dst, uint32_t nb, uint32_t nd = 0) {
     pending_dst.push_back(dst);
     pending_nb.push_back(nb);
+    pending_nd.push_back(nd);
   }
   const char* flush() {
     size_t i = 0;
@@ -245,18 +324,35 @@ struct Ctx {
       // group consecutive slots with equal partial counts into one launch
       size_t j = i;
       fin_table tab{};
-      while (j < pending_dst.size() && pending_nb[j] == pending_nb[i]) {
+      while (j < pending_dst.size() && pending_nb[j] == pending_nb[i] &&
+             pending_nd[j] == pending_nd[i]) {
         tab.dst[j - i] = pending_dst[j];
         ++j;
+      }
+      const cx* p2 = dparts + i * (size_t)DYN_CAP * RED;
+      uint64_t s2 = (uint64_t)DYN_CAP * RED;
+      uint32_t n2 = pending_nd[i];
+      if (n2 > (uint32_t)BLOCK) {  // many granules: pre-sum them in chunks of BLOCK (fixed order)
+        const uint32_t nch = (n2 + BLOCK - 1) / BLOCK;
+        const uint64_t os = (uint64_t)(DYN_CAP / BLOCK) * RED;
+        cx* out = dsums + i * (size_t)(DYN_CAP / BLOCK) * RED;
+        hipLaunchKernelGGL(k_dsum, dim3(nch, (uint32_t)(j - i)), dim3(BLOCK), 0, stream, p2, s2,
+                           n2, out, os);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail("HIP ERROR: launch of kernel dsum failed with %s.", hipGetErrorName(e));
+        p2 = out;
+        s2 = os;
+        n2 = nch;
       }
       QDC_TRY(launch("finalize", 0.0, k_finalize,
                      (uint32_t)(j - i), (const cx*)(partials + i * (size_t)NBMAX * RED),
                      (uint64_t)NBMAX * RED, pending_nb[i], tab, pending_base,
-                     pending_accumulate));
+                     pending_accumulate, p2, s2, n2));
       i = j;
     }
     pending_dst.clear();
     pending_nb.clear();
+    pending_nd.clear();
     return nullptr;
   }
 };

@@ -552,17 +552,35 @@ struct fin_table {
   uint32_t dst[FIN_MAX];
 };
 
+// Granule partials of a dynamic-tail pass, pre-summed: block (slot y, chunk x) adds the BLOCK
+// partials x*BLOCK .. of slot y by a fixed tree (block_reduce_store) into one chunk partial.
+__global__ __launch_bounds__(BLOCK) void k_dsum(const cx* __restrict__ parts, uint64_t stride,
+                                                uint32_t n, cx* __restrict__ out,
+                                                uint64_t out_stride) {
+  const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const cx* p = parts + (uint64_t)blockIdx.y * stride + g * RED;
+  cx acc[RED];
+#pragma unroll
+  for (int k = 0; k < RED; ++k) acc[k] = g < n ? p[k] : cx{0, 0};
+  block_reduce_store<RED>(acc, out + (uint64_t)blockIdx.y * out_stride + (uint64_t)blockIdx.x * RED);
+}
+
+// one slot per block: the sum of its nblocks block partials, then of its n2 granule partials
+// (dynamic-tail passes, fgeo::dpart) — a fixed order, so the result is deterministic
 __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ partials,
                                                     uint64_t slot_stride, uint32_t nblocks,
                                                     fin_table tab, cx* __restrict__ dst,
-                                                    int accumulate) {
+                                                    int accumulate, const cx* __restrict__ partials2,
+                                                    uint64_t slot_stride2, uint32_t n2) {
   const cx* p = partials + (uint64_t)blockIdx.x * slot_stride;
+  const cx* p2 = partials2 + (uint64_t)blockIdx.x * slot_stride2;
   cx acc[RED];
 #pragma unroll
   for (int k = 0; k < RED; ++k) acc[k] = {0, 0};
-  for (uint32_t blk = threadIdx.x; blk < nblocks; blk += BLOCK) {
+  for (uint32_t blk = threadIdx.x; blk < nblocks + n2; blk += BLOCK) {
+    const cx* q = blk < nblocks ? p + (uint64_t)blk * RED : p2 + (uint64_t)(blk - nblocks) * RED;
 #pragma unroll
-    for (int k = 0; k < RED; ++k) acc[k] = cadd(acc[k], p[(uint64_t)blk * RED + k]);
+    for (int k = 0; k < RED; ++k) acc[k] = cadd(acc[k], q[k]);
   }
   __shared__ cx out[RED];
   block_reduce_store<RED>(acc, out);
@@ -621,7 +639,32 @@ struct fgeo {
   uint32_t order;  // register-resident passes: 0 block-contiguous tiles, 1 grid-strided
   uint64_t gm;     // gap mask (geo::gm); register-resident passes get their rqio offsets gapped
                    // on the host, so only the tile base is gapped here
+  // Dynamic tail (one-wave register-resident passes, k_rw): blocks run tpb block-contiguous
+  // tiles of the first nstat, then take tiles [nstat, nstat + ndyn) one at a time from eight
+  // atomic counters (pool p = block % 8, the blocks of one XCD, owns ndyn / 8 of them), so a
+  // wave that finished its static share early keeps its SIMD busy instead of leaving the partner
+  // wave alone (SQ counters: waves lived 81 % of the reverse pass with static shares only).
+  // ndyn = 0: static only.
+  unsigned long long* dctr;  // 8 counters, FG_DCTR_STRIDE apart (own cache lines)
+  uint64_t dbase;            // value of every counter at this launch's start (all advance alike)
+  uint64_t nstat, ndyn;
+  uint32_t dgran;            // tiles per grab (a granule); ndyn is a multiple of 8 dgran
+  // Reductions stay deterministic: the static tiles of a block sum into its block partial; each
+  // granule's Gamma sums go to its own partial, dpart[slot * dstride + granule * RED], so every
+  // value is summed over the same tiles in the same order whichever wave ran them
+  cx* dpart;
+  uint64_t dstride;
 };
+constexpr int FG_DCTR_STRIDE = 32;  // 256 B between the pool counters
+
+// next tile index of this block's pool (>= ndyn / 8: the pool is empty); one wave per block
+__device__ __forceinline__ uint64_t fg_grab(const fgeo& fg) {
+  unsigned long long v = 0;
+  if (threadIdx.x == 0) v = atomicAdd(fg.dctr + FG_DCTR_STRIDE * (blockIdx.x & 7u), 1ull);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((((uint64_t)hi) << 32) | lo) - fg.dbase;
+}
 
 // Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the
 // natural (re, im) register pairs, with op_sel/neg modifiers doing the broadcast and swap:

@@ -664,10 +664,12 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x
                                  : (uint64_t)xcd_block(blockIdx.x, gridDim.x, fg.order == 2) * fg.tpb;
   const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
+  // the static share: all tiles (ndyn = 0), or the block's tpb of the first nstat
+  const uint64_t nst = fg.ndyn ? fg.nstat : fg.ntiles;
   const uint32_t count =
-      tile0 >= fg.ntiles ? 0u
-      : gstride          ? (uint32_t)((fg.ntiles - 1 - tile0) / tstep + 1)
-                         : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+      tile0 >= nst ? 0u
+      : gstride    ? (uint32_t)((nst - 1 - tile0) / tstep + 1)
+                   : (uint32_t)min<uint64_t>(fg.tpb, nst - tile0);
   auto tile_base = [&](uint64_t tile) {
     uint64_t base = tile << fg.lc;
 #pragma unroll
@@ -800,17 +802,43 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       if (gamma) ++ri;
     }
   };
+  // Gamma sums so far to dst[k * stride + e] (slot k), accumulators re-zeroed (dynamic tail)
+  auto flush_acc = [&](cx* dst, uint64_t stride) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < fg.ngrad * FACC; i += 64) {
+      const uint32_t k = i / FACC, e = i % FACC;
+      reinterpret_cast<real*>(dst + (uint64_t)k * stride)[e] = accw[k][e];
+      accw[k][e] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
   cx xf[R], xb[R];  // xb unused (eliminated) in one-state passes
   if constexpr (!PF) {
     if (QDC_RQ_ABL & 32) {  // timing-only: no HBM traffic (registers start from the lane id)
 #pragma unroll
       for (int j = 0; j < R; ++j) xf[j] = xb[j] = cx{(real)(lane + j) * 1e-3f, (real)j * 1e-3f};
     }
-    for (uint32_t tt = 0; tt < count; ++tt) {
-      const uint64_t base = tile_base(tile0 + tt * tstep);
+    auto tile = [&](uint64_t t) __attribute__((always_inline)) {
+      const uint64_t base = tile_base(t);
       if (!(QDC_RQ_ABL & 32)) load(xf, xb, base);
       run(xf, xb);
       if (!(QDC_RQ_ABL & 32) || base == ~0ull) store(xf, xb, base);
+    };
+    for (uint32_t tt = 0; tt < count; ++tt) tile(tile0 + tt * tstep);
+    if constexpr (W == 1) {
+      if (fg.ndyn) {  // dynamic tail: this block's pool, one granule of dgran tiles per grab
+        // the static tiles' Gamma sums are this block's partial; each granule gets its own
+        if constexpr (TWO) flush_acc(partials + (uint64_t)blockIdx.x * RED, slot_stride);
+        const uint64_t per = fg.ndyn / (8ull * fg.dgran);  // granules per pool
+        const uint32_t pool = blockIdx.x & 7u;
+        for (;;) {
+          const uint64_t k = fg_grab(fg);
+          if (k >= per) break;
+          const uint64_t gi = (uint64_t)pool * per + k;  // granule index in [0, ndyn / dgran)
+          for (uint32_t t = 0; t < fg.dgran; ++t) tile(fg.nstat + gi * fg.dgran + t);
+          if constexpr (TWO) flush_acc(fg.dpart + gi * RED, fg.dstride);
+        }
+      }
     }
   } else {
     static_assert(TWO && NE == 2, "k_rw prefetch: two-state tiles (32 chunks in a[0:127])");
@@ -858,11 +886,14 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     }
   }
   if constexpr (TWO) {
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < fg.ngrad * FACC; i += 64) {
-      const uint32_t k = i / FACC, e = i % FACC;
-      reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] =
-          accw[k][e];
+    // (a dynamic-tail pass wrote the block partial after its static tiles)
+    if (PF || W != 1 || !fg.ndyn) {
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = lane; i < fg.ngrad * FACC; i += 64) {
+        const uint32_t k = i / FACC, e = i % FACC;
+        reinterpret_cast<real*>(partials + (uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED)[e] =
+            accw[k][e];
+      }
     }
   }
 }

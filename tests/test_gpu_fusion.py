@@ -272,3 +272,51 @@ def test_f64_register_resident_passes_equal_lds_passes(case):
         fl.check("uncomputed", c.get_state(0), what)
         res[rq64] = g
     F.check_pair("f64", res[1], res[0], fl.floor["grads"], f"{case} f64 k_rw vs lds grads")
+
+
+def _with_env(env, make):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return make()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_dynamic_tail_is_deterministic(prec):
+    """Reverse passes with a dynamic tail (tiles handed out by atomic counters, so which wave
+    runs which tile changes from run to run) give bit-identical densities, gradients and states
+    on every call: each granule of dynamic tiles reduces into its own partial, summed in a fixed
+    order (qdc_rq.hpp k_rw, k_dsum, k_finalize).  Against static shares only (QDC_DYN=100) the
+    results differ by rounding: within the north star's tolerance."""
+    import quantum_differentiable_circuit as q
+    n = 24 if prec == "f32" else 23  # >= 4 x 2048 tiles, so the tail is on
+    ins, var = O.layered_circuit(n, layers=2, seed=5)
+    dt = DT[prec]
+    vg = [np.ascontiguousarray(g, dtype=dt) for g in var]
+    cots = F.sigma_z_cots([np.zeros((2, 2))] * n, dt)
+
+    def once(env):
+        c = _with_env(env, lambda: q.circuit_class(prec)(n))
+        for kind, pos in ins:
+            c._push(kind, *pos)
+        d = c.forward([], vg)
+        g = c.backward(cots, [], vg)
+        d2 = c.forward([], vg)
+        g2 = c.backward(cots, [], vg)
+        return np.concatenate([x.reshape(-1) for x in d]), np.concatenate(g), \
+            np.concatenate([x.reshape(-1) for x in d2]), np.concatenate(g2), c.get_state(2)
+
+    d1, g1, d1b, g1b, b1 = once({"QDC_DYN": "35"})
+    assert np.array_equal(d1, d1b) and np.array_equal(g1, g1b), "repeat calls differ"
+    d2, g2, _, _, b2 = once({"QDC_DYN": "35"})
+    assert np.array_equal(g1, g2) and np.array_equal(b1, b2), "two circuits differ"
+    d3, g3, _, _, _ = once({"QDC_DYN": "100"})
+    tol = 1e-5 if prec == "f32" else 1e-12
+    assert F.normrel(g3, g1) <= tol and F.normrel(d3, d1) <= tol
+    print(f"[dyn] {prec} n={n}: static-only vs dynamic tail, grads {F.normrel(g3, g1):.2e}")
