@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--local-shards", type=int, default=None,
                     help="rehearse the sharded data path on one GPU (G shards, device copies in "
                          "place of the RCCL all-to-all); not a multi-GPU measurement")
+    ap.add_argument("--local-streams", type=int, default=None,
+                    help="rehearse the single-process multi-GPU path on one GPU: G shards, each "
+                         "on its own stream of device 0 (event-ordered copies in place of RCCL)")
     ap.add_argument("--no-gate-sample", action="store_true",
                     help="skip the single-gate (fusion off) kernel sample")
     ap.add_argument("--cpu-gates", type=int, default=12,
@@ -525,6 +528,8 @@ def main():
         comm = Communicator(args.precision, rank=rank, world=world, device=local)
     elif args.gpus > 1:  # one plain process driving every GPU (ncclCommInitAll)
         devices = list(range(args.gpus))
+    elif args.local_streams and args.local_streams > 1:  # the same plumbing, one GPU
+        devices = [0] * args.local_streams
     c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision, comm,
                                args.local_shards, devices)
     ngates = len(vg)
@@ -600,7 +605,7 @@ def main():
     # the fused path against the per-gate roofline: every gate costs 2S forward and 4S in the
     # reverse sweep (SURVEY.md §8 d) if applied one HBM pass at a time
     state_bytes = (1 << n) * (8 if args.precision == "f32" else 16)
-    ngpu = world if world > 1 else (len(devices) if devices else 1)
+    ngpu = world if world > 1 else (len(set(devices)) if devices else 1)
     eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / ngpu
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
@@ -647,6 +652,9 @@ def main():
                                        f"RCCL all-to-all remaps, one process per GPU") if world > 1 else
                                       (f"state sharded over {ngpu} GPUs by high qubits, RCCL "
                                        f"all-to-all remaps, one process (ncclCommInitAll)")
+                                      if devices and ngpu > 1 else
+                                      (f"rehearsal: {len(devices)} shards on one GPU, one stream "
+                                       f"each (event-ordered device copies)")
                                       if devices else
                                       (f"rehearsal: {shards} shards on one GPU (device copies)"
                                        if shards > 1 else "single GPU"),

@@ -1093,10 +1093,14 @@ struct Circuit {
     uint32_t grid = 0;
     QDC_TRY(fused_grid(fg, kern, (int)nt, grid));
     fgeo g = fg;
-    uint64_t tpb = 1;
-    while (tpb * grid < g.ntiles) tpb <<= 1;
-    g.tpb = (uint32_t)tpb;
-    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    // one-state prefetching passes: static shares + a dynamic tail (no reductions here)
+    if (!(!two && pf && g.ngrad == 0 && grid >= 8 && g.ntiles >= 4ull * grid &&
+          ctx.plan_dyn(g, grid))) {
+      uint64_t tpb = 1;
+      while (tpb * grid < g.ntiles) tpb <<= 1;
+      g.tpb = (uint32_t)tpb;
+      grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    }
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
     last_fused_ndyn = 0;

@@ -208,7 +208,7 @@ struct Ctx {
   // granule partials of a reducing pass within DYN_CAP per slot.
   bool plan_dyn(fgeo& g, uint32_t grid) {
     last_ndyn = 0;
-    if (!dctr || dyn_static_pct >= 100 || (grid & 7u) || (g.ntiles & 7u) || g.order == 1)
+    if (!QDC_DYN_TAIL || !dctr || dyn_static_pct >= 100 || (grid & 7u) || (g.ntiles & 7u) || g.order == 1)
       return false;
     if (g.ngrad > 0 && !dparts) {  // first reducing dynamic pass of this context
       if (hipMalloc(&dparts, sizeof(cx) * (size_t)FIN_MAX * DYN_CAP * RED) != hipSuccess ||

@@ -29,6 +29,8 @@
 // symbols, so there is no cross-thread race (README.md:13).
 #pragma once
 
+#include <cstddef>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -656,14 +658,39 @@ struct fgeo {
   uint64_t dstride;
 };
 constexpr int FG_DCTR_STRIDE = 32;  // 256 B between the pool counters
+// dynamic tails compiled in (0: static shares only; Ctx::plan_dyn then never plans one)
+#ifndef QDC_DYN_TAIL
+#define QDC_DYN_TAIL 1
+#endif
+
+// The fgeo argument of the register-resident kernels (k_rq, k_rw: four pointers precede it),
+// read through an opaque kernarg-segment pointer: the dynamic-tail fields are used once per
+// grab, so they are loaded (s_load, scalar cache) at their uses instead of being held in SGPRs
+// across the pass — held, they pushed the reverse kernel's SGPR spills from 27 to 57.
+struct fg_kernargs {  // the kernels' leading parameters, as the kernarg segment lays them out
+  void* f;
+  void* b;
+  const void* ops;
+  const void* mats;
+  fgeo fg;
+};
+constexpr size_t FG_KERNARG_OFFSET = offsetof(fg_kernargs, fg);
+static_assert(FG_KERNARG_OFFSET == 32, "fgeo follows four pointers");
+typedef const __attribute__((address_space(4))) fgeo* fg_kptr;
+__device__ __forceinline__ fg_kptr fg_arg() {
+  const __attribute__((address_space(4))) char* p =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (fg_kptr)(p + FG_KERNARG_OFFSET);
+}
 
 // next tile index of this block's pool (>= ndyn / 8: the pool is empty); one wave per block
-__device__ __forceinline__ uint64_t fg_grab(const fgeo& fg) {
+__device__ __forceinline__ uint64_t fg_grab() {
   unsigned long long v = 0;
-  if (threadIdx.x == 0) v = atomicAdd(fg.dctr + FG_DCTR_STRIDE * (blockIdx.x & 7u), 1ull);
+  if (threadIdx.x == 0) v = atomicAdd(fg_arg()->dctr + FG_DCTR_STRIDE * (blockIdx.x & 7u), 1ull);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((((uint64_t)hi) << 32) | lo) - fg.dbase;
+  return ((((uint64_t)hi) << 32) | lo) - fg_arg()->dbase;
 }
 
 // Complex multiply(-accumulate) for the fused kernels.  In f32 each is two v_pk_fma_f32 on the

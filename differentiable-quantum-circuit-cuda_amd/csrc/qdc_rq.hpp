@@ -447,10 +447,12 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   const uint64_t tile0 = gstride ? (uint64_t)blockIdx.x
                                  : (uint64_t)xcd_block(blockIdx.x, gridDim.x, fg.order == 2) * fg.tpb;
   const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
+  // static share (all tiles, or tpb of the first nstat with a dynamic tail: one-state PF only)
+  const uint64_t nst = (QDC_DYN_TAIL && PF && !TWO && fg_arg()->ndyn) ? fg_arg()->nstat : fg.ntiles;
   const uint32_t count =
-      tile0 >= fg.ntiles ? 0u
-      : gstride          ? (uint32_t)((fg.ntiles - 1 - tile0) / tstep + 1)
-                         : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+      tile0 >= nst ? 0u
+      : gstride    ? (uint32_t)((nst - 1 - tile0) / tstep + 1)
+                   : (uint32_t)min<uint64_t>(fg.tpb, nst - tile0);
   auto tile_base = [&](uint64_t tile) {
     uint64_t base = tile << fg.lc;
 #pragma unroll
@@ -575,12 +577,48 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         }
       }
     };
+    // Dynamic tail (one-state passes, fgeo::ndyn): after its count static tiles the block takes
+    // tiles from its pool's counter.  Thread 0 grabs step s+1's tile during step s — the atomic
+    // is older than that step's stores, so the compiler's own wait for its result is vmcnt(#
+    // stores) and never drains the pipeline — and hands it to the block through LDS.
+    __shared__ uint64_t grab_sh;
+    unsigned long long grabbed = 0;  // thread 0: the counter value of the grab in flight
+    const bool dyn = QDC_DYN_TAIL && !TWO && fg_arg()->ndyn != 0;
+    const uint64_t per = dyn ? fg_arg()->ndyn >> 3 : 0;
+    const uint64_t pool0 = fg_arg()->nstat + (uint64_t)(blockIdx.x & 7u) * per;
+    auto grab_issue = [&]() __attribute__((always_inline)) {
+      if (t == 0) grabbed = atomicAdd(fg_arg()->dctr + FG_DCTR_STRIDE * (blockIdx.x & 7u), 1ull);
+    };
+    auto grab_take = [&]() __attribute__((always_inline)) {  // block-uniform: k-th pool tile
+      __syncthreads();  // every thread read the previous grab
+      if (t == 0) grab_sh = (uint64_t)grabbed - fg_arg()->dbase;
+      __syncthreads();
+      const uint64_t k = grab_sh;
+      return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(k >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)k);
+    };
+    bool more = true;  // a further tile may come (block-uniform)
+    if (dyn && count == 0) grab_issue();
+    // tile of step s, or false: none (the block's last grab, which found its pool empty)
+    auto next = [&](uint32_t s, uint64_t& tile) __attribute__((always_inline)) {
+      if (s < count) {
+        tile = tile0 + s * tstep;
+        if (dyn && s + 1 == count) grab_issue();  // the first dynamic tile, one step ahead
+        return true;
+      }
+      if (!dyn) return false;
+      const uint64_t k = grab_take();
+      if (k >= per) return false;
+      tile = pool0 + k;
+      grab_issue();
+      return true;
+    };
     // Step s takes tile s-1 (loaded during step s-1), issues tile s, runs and stores tile s-1.
     // One issue site: the in-flight registers are a loop-carried value with an undefined entry,
     // so the register allocator has no phi copies to place (a copy before the wait would read
     // in-flight registers; tools/check_rq_isa.py checks the ISA for exactly that).
     uint64_t cur = 0;
-    for (uint32_t s = 0; s <= count; ++s) {
+    for (uint32_t s = 0;; ++s) {
       // younger than tile s-1's loads: tile s-2's stores (none before the second tile; at s = 0
       // nothing is in flight and take() reads registers nothing uses).  Unconditional, so every
       // path from an issue to the next read of its registers passes this wait.
@@ -590,14 +628,18 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         rq_vmwait_one<NLD>(s <= 1 ? 1u : 0u, pf_f);
       take();
       const uint64_t prev = cur;
-      if (s < count) {
-        cur = tile_base(tile0 + s * tstep);
+      uint64_t tile = 0;
+      if (more && next(s, tile)) {
+        cur = tile_base(tile);
         issue(cur);
+      } else {
+        more = false;
       }
       if (s > 0) {
         run(xf, xb);
         store(xf, xb, prev);
       }
+      if (!more) break;
     }
   }
   if constexpr (TWO) {
@@ -665,7 +707,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
                                  : (uint64_t)xcd_block(blockIdx.x, gridDim.x, fg.order == 2) * fg.tpb;
   const uint64_t tstep = gstride ? (uint64_t)gridDim.x : 1u;
   // the static share: all tiles (ndyn = 0), or the block's tpb of the first nstat
-  const uint64_t nst = fg.ndyn ? fg.nstat : fg.ntiles;
+  const uint64_t nst = (QDC_DYN_TAIL && fg_arg()->ndyn) ? fg_arg()->nstat : fg.ntiles;
   const uint32_t count =
       tile0 >= nst ? 0u
       : gstride    ? (uint32_t)((nst - 1 - tile0) / tstep + 1)
@@ -824,21 +866,37 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       run(xf, xb);
       if (!(QDC_RQ_ABL & 32) || base == ~0ull) store(xf, xb, base);
     };
-    for (uint32_t tt = 0; tt < count; ++tt) tile(tile0 + tt * tstep);
-    if constexpr (W == 1) {
-      if (fg.ndyn) {  // dynamic tail: this block's pool, one granule of dgran tiles per grab
-        // the static tiles' Gamma sums are this block's partial; each granule gets its own
-        if constexpr (TWO) flush_acc(partials + (uint64_t)blockIdx.x * RED, slot_stride);
-        const uint64_t per = fg.ndyn / (8ull * fg.dgran);  // granules per pool
-        const uint32_t pool = blockIdx.x & 7u;
-        for (;;) {
-          const uint64_t k = fg_grab(fg);
+    // The static share, then (W = 1, fgeo::ndyn) the dynamic tail: this block's pool, one
+    // granule of dgran tiles per grab.  The static tiles' Gamma sums are this block's partial,
+    // each granule's go to its own (written when the next grab is due).  One loop, one call
+    // site of the tile body (a second copy of it raised the spills).
+    const bool dyn = QDC_DYN_TAIL && W == 1 && fg_arg()->ndyn != 0;
+    const uint64_t per = dyn ? fg_arg()->ndyn / (8ull * fg_arg()->dgran) : 0;  // granules per pool
+    uint32_t tt = 0, gleft = 0;
+    uint64_t gi = ~0ull;  // current granule (~0: none yet)
+    for (;;) {
+      uint64_t t;
+      if (tt < count) {
+        t = tile0 + tt * tstep;
+        ++tt;
+      } else {
+        if (!dyn) break;
+        if (gleft == 0) {
+          if constexpr (TWO) {
+            if (gi == ~0ull)
+              flush_acc(partials + (uint64_t)blockIdx.x * RED, slot_stride);
+            else
+              flush_acc(fg_arg()->dpart + gi * RED, fg_arg()->dstride);
+          }
+          const uint64_t k = fg_grab();
           if (k >= per) break;
-          const uint64_t gi = (uint64_t)pool * per + k;  // granule index in [0, ndyn / dgran)
-          for (uint32_t t = 0; t < fg.dgran; ++t) tile(fg.nstat + gi * fg.dgran + t);
-          if constexpr (TWO) flush_acc(fg.dpart + gi * RED, fg.dstride);
+          gi = (uint64_t)(blockIdx.x & 7u) * per + k;  // granule index in [0, ndyn / dgran)
+          gleft = fg_arg()->dgran;
         }
+        t = fg_arg()->nstat + gi * fg_arg()->dgran + (fg_arg()->dgran - gleft);
+        --gleft;
       }
+      tile(t);
     }
   } else {
     static_assert(TWO && NE == 2, "k_rw prefetch: two-state tiles (32 chunks in a[0:127])");
@@ -887,7 +945,7 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
   }
   if constexpr (TWO) {
     // (a dynamic-tail pass wrote the block partial after its static tiles)
-    if (PF || W != 1 || !fg.ndyn) {
+    if (PF || W != 1 || !QDC_DYN_TAIL || !fg_arg()->ndyn) {
       __builtin_amdgcn_wave_barrier();
       for (uint32_t i = lane; i < fg.ngrad * FACC; i += 64) {
         const uint32_t k = i / FACC, e = i % FACC;
