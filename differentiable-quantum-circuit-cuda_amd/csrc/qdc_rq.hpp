@@ -453,12 +453,16 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       tile0 >= nst ? 0u
       : gstride    ? (uint32_t)((nst - 1 - tile0) / tstep + 1)
                    : (uint32_t)min<uint64_t>(fg.tpb, nst - tile0);
+  // (geometry read through the kernarg pointer at each use: held in SGPRs across the pass it was
+  // spilled to VGPR lanes and this ran on the VALU)
   auto tile_base = [&](uint64_t tile) {
-    uint64_t base = tile << fg.lc;
+    const fg_kptr a = fg_arg();
+    uint64_t base = tile << a->lc;
+    const uint32_t h = a->h;
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
-      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    return base + (base & fg.gm);
+      if ((uint32_t)k < h) base = insert_zero(base, a->hb[k]);
+    return base + (base & a->gm);
   };
   // re-read per use, so the compiler does not hold the offsets in SGPRs across the pass
   auto rqio_now = [&]() {
@@ -712,12 +716,16 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       tile0 >= nst ? 0u
       : gstride    ? (uint32_t)((nst - 1 - tile0) / tstep + 1)
                    : (uint32_t)min<uint64_t>(fg.tpb, nst - tile0);
+  // (geometry read through the kernarg pointer at each use: held in SGPRs across the pass it was
+  // spilled to VGPR lanes and this ran on the VALU)
   auto tile_base = [&](uint64_t tile) {
-    uint64_t base = tile << fg.lc;
+    const fg_kptr a = fg_arg();
+    uint64_t base = tile << a->lc;
+    const uint32_t h = a->h;
 #pragma unroll
     for (int k = 0; k < FMAX_ROWS; ++k)
-      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
-    return base + (base & fg.gm);
+      if ((uint32_t)k < h) base = insert_zero(base, a->hb[k]);
+    return base + (base & a->gm);
   };
   auto rqio_now = [&]() {
     uint32_t ro = l0;

@@ -159,3 +159,45 @@ def test_devices_rccl_single_process():
     c = build(q, "f64", n, ins, devices=2)
     fl.check("forward", c.forward([], fl.var), "devices=2 ")
     fl.check("grads", c.backward(fl.cots, [], fl.var), "devices=2 ")
+
+
+def _current_device():
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    d = ctypes.c_int(-1)
+    assert hip.hipGetDevice(ctypes.byref(d)) == 0
+    return d.value
+
+
+def _set_device(i):
+    import ctypes
+    assert ctypes.CDLL("libamdhip64.so").hipSetDevice(ctypes.c_int(i)) == 0
+
+
+def test_entry_points_keep_the_callers_device():
+    """Every circuit entry point leaves the caller's HIP device current (qdc::DeviceGuard): a
+    multi-device circuit switches devices per shard, and the C-ABI primitives, torch and the
+    caller's code must not find themselves on the last shard's GPU afterwards.  On one GPU the
+    repeated-device circuit covers the per-shard contexts; with two GPUs the circuit lives on
+    device 1 while the caller stays on device 0 (and the reverse)."""
+    import torch
+    import quantum_differentiable_circuit as q
+    n = 10
+    ins, var = O.layered_circuit(n, layers=1, seed=3)
+    vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
+    cots = F.sigma_z_cots([np.zeros((2, 2))] * n, np.complex64)
+    cases = [([0, 0], 0)]
+    if torch.cuda.device_count() >= 2:
+        cases += [([1], 0), ([0], 1), ([0, 1], 1)]
+    for devs, caller in cases:
+        _set_device(caller)
+        c = build(q, "f32", n, ins, devices=devs)
+        assert _current_device() == caller, f"constructor moved the caller ({devs})"
+        c.forward([], vg)
+        c.backward(cots, [], vg)
+        c.get_state(0)
+        c.synchronize()
+        assert _current_device() == caller, f"forward/backward moved the caller ({devs})"
+        del c
+        assert _current_device() == caller, f"destructor moved the caller ({devs})"
+    _set_device(0)
