@@ -232,6 +232,9 @@ struct Circuit {
   int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
   int rq64 = 1;  // f64 gate passes register-resident too (k_rw; QDC_RQ64)
   int rq_slots5 = 1;  // two-state f32 k_rw passes plan five register slots (QDC_RQ_SLOTS5)
+  // one-state f32 passes on 2^12 tiles run on two-wave, five-slot, prefetching k_rw tiles
+  // instead of four-wave, four-slot k_rq ones (QDC_RQ_FWD5)
+  int rq_fwd5 = 0;  // measured 4 % slower per pass (r3i): 16 KiB of LDS per wave caps it at 2 waves/SIMD
   bool rq5() const { return rq_slots5 != 0 && (rq_wave & 1) && !(rq_wave & 4); }
   // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
   // XCD-aware block order (QDC_RQ_ORDER)
@@ -301,6 +304,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_ORDER")) rq_order = atoi(e);
     if (const char* e = getenv("QDC_RQ64")) rq64 = atoi(e);
     if (const char* e = getenv("QDC_RQ_SLOTS5")) rq_slots5 = atoi(e);
+    if (const char* e = getenv("QDC_RQ_FWD5")) rq_fwd5 = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
@@ -935,7 +939,8 @@ struct Circuit {
       }
       // five register slots on the one-wave two-state f32 kernel (k_rw<.., S5>)
       const bool s5_two = two && rq5();
-      const bool s5_one = !two && rq_slots5 && (rq_wave & 2) && it.tbits == 11;  // k_rw W = 1
+      const bool s5_one = !two && ((rq_slots5 && (rq_wave & 2) && it.tbits == 11) ||  // k_rw W = 1
+                                   (rq_fwd5 && it.tbits == 12));  // k_rw W = 2, prefetching
       const uint32_t ns = (sizeof(real) == 4 && (s5_two || s5_one)) ? 5u : 4u;
       it.s5 = ns == 5;
       const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
@@ -1039,6 +1044,22 @@ struct Circuit {
                         const cx* mats, cx* partials, uint64_t stride, bool s5) {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
+    if (!two && s5 && nt == 256) {  // two waves per 2^12 tile, five slots, prefetching
+      const void* kw = (const void*)k_rw<false, 2, true, 2, true>;
+      uint32_t grid = 0;
+      QDC_TRY(fused_grid(fg, kw, 128, grid));
+      fgeo g = fg;
+      if (!(g.ngrad == 0 && grid >= 8 && g.ntiles >= 4ull * grid && ctx.plan_dyn(g, grid))) {
+        uint64_t tpb = 1;
+        while (tpb * grid < g.ntiles) tpb <<= 1;
+        g.tpb = (uint32_t)tpb;
+        grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+      }
+      last_fused_grid = grid;
+      last_fused_ndyn = 0;
+      return ctx.launch_block(name, bytes, k_rw<false, 2, true, 2, true>, grid, 128u, f, b, fops,
+                              mats, g, l0, partials, stride);
+    }
     if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
       // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);

@@ -676,13 +676,19 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 // S5: five-slot layouts (NE = 2, W = 1): the register-group bit is register slot 4, which
 // stages address like the other four, so covers hold 5 qubits (fewer relayouts); the layout
 // descriptor then spans all 32 registers (rp[16 e + j], chunk offsets offi[8 e + i]).
+// One-state forward passes on 2^12-amplitude tiles (round 3): W = 2, NE = 2, S5 and PF — two
+// waves per tile, 32 amplitudes per lane, five register slots (k_rq's one-state tiles hold 16
+// per thread: four slots, and a third of the forward's VALU time went to relayouts with their
+// four-wave barriers), and the next tile's 16 chunks per lane prefetched into pinned VGPRs as in
+// k_rq (rq_ld / rq_vmwait_two), with a dynamic tail taken block-wide.
 template <bool TWO, int NE, bool PF, int W, bool S5 = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PF ? 1 : QDC_RW_WAVES, PF ? 1 : QDC_RW_WAVES)))
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu((PF && TWO) ? 1 : QDC_RW_WAVES, (PF && TWO) ? 1 : QDC_RW_WAVES)))
 void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
   static_assert(NE == 1 || NE == 2 || NE == 4, "k_rw: 1, 2 or 4 register groups");
-  static_assert(!S5 || (NE == 2 && W == 1 && VEC == 2 && !PF), "five slots: f32 one-wave tiles");
+  static_assert(!S5 || (NE == 2 && VEC == 2 && ((W == 1 && !PF) || (W == 2 && PF && !TWO))),
+                "five slots: f32 one-wave tiles, or the two-wave prefetching one-state tiles");
   static_assert(W == 1 || (W == 2 && !TWO), "k_rw: two-state tiles are one wave");
   constexpr int LOGNE = NE == 1 ? 0 : NE == 2 ? 1 : 2;
   constexpr int TB = W == 1 ? 6 : 7;  // k_rq thread bits held by the block's threads
@@ -905,6 +911,84 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
         --gleft;
       }
       tile(t);
+    }
+  } else if constexpr (!TWO) {
+    // one-state prefetch (W = 2, NE = 2, S5): this lane's 16 chunks of the next tile in flight in
+    // pinned v[192:255] while this tile runs; step s takes tile s-1, issues tile s, runs and
+    // stores tile s-1 (k_rq's PF loop, with k_rw's register groups)
+    static_assert(NE == 2 && W == 2 && S5 && CPT == 16, "one-state prefetch: 2^12 S5 tiles");
+    constexpr int NLD = CPT;  // vector-memory ops per tile: loads = stores
+    vec16 pf_a[8], pf_b[8];   // chunks 0..7 (register group 0) and 8..15 (group 1)
+    auto issue = [&](uint64_t base) __attribute__((always_inline)) {
+      const rqio* rg = rqio_now();
+      const chunk* pfp = f + (base + thr_ld);
+#define QDC_RW1_ISSUE(i)                                             \
+  pf_a[i] = rq_ld<RQ_PIN_TWO + 4 * (i)>(pfp + rg->offi_ld[i]);       \
+  pf_b[i] = rq_ld<RQ_PIN_TWO + 32 + 4 * (i)>(pfp + rg->offi_ld[8 + (i)]);
+      QDC_RW1_ISSUE(0) QDC_RW1_ISSUE(1) QDC_RW1_ISSUE(2) QDC_RW1_ISSUE(3)
+      QDC_RW1_ISSUE(4) QDC_RW1_ISSUE(5) QDC_RW1_ISSUE(6) QDC_RW1_ISSUE(7)
+#undef QDC_RW1_ISSUE
+    };
+    auto take = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const chunk c = __builtin_bit_cast(chunk, pf_a[i]);
+        const chunk d = __builtin_bit_cast(chunk, pf_b[i]);
+        xf[2 * i] = c.v[0];
+        xf[2 * i + 1] = c.v[1];
+        xf[16 + 2 * i] = d.v[0];
+        xf[16 + 2 * i + 1] = d.v[1];
+      }
+    };
+    // dynamic tail, block-wide: thread 0 grabs step s+1's tile during step s (older than that
+    // step's stores: the compiler's own wait for it is vmcnt(stores)), the block reads it from LDS
+    __shared__ uint64_t grab_sh;
+    unsigned long long grabbed = 0;
+    const bool dyn = QDC_DYN_TAIL && fg_arg()->ndyn != 0;
+    const uint64_t per = dyn ? fg_arg()->ndyn >> 3 : 0;
+    auto grab_issue = [&]() __attribute__((always_inline)) {
+      if (lane == 0) grabbed = atomicAdd(fg_arg()->dctr + FG_DCTR_STRIDE * (blockIdx.x & 7u), 1ull);
+    };
+    auto grab_take = [&]() __attribute__((always_inline)) {
+      __syncthreads();
+      if (lane == 0) grab_sh = (uint64_t)grabbed - fg_arg()->dbase;
+      __syncthreads();
+      const uint64_t k = grab_sh;
+      return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(k >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)k);
+    };
+    if (dyn && count == 0) grab_issue();
+    auto next = [&](uint32_t s, uint64_t& t) __attribute__((always_inline)) {
+      if (s < count) {
+        t = tile0 + s * tstep;
+        if (dyn && s + 1 == count) grab_issue();
+        return true;
+      }
+      if (!dyn) return false;
+      const uint64_t k = grab_take();
+      if (k >= per) return false;
+      t = fg_arg()->nstat + (uint64_t)(blockIdx.x & 7u) * per + k;
+      grab_issue();
+      return true;
+    };
+    bool more = true;
+    uint64_t cur = 0;
+    for (uint32_t s = 0;; ++s) {
+      rq_vmwait_two<NLD>(s <= 1 ? 1u : 0u, pf_a, pf_b);
+      take();
+      const uint64_t prev = cur;
+      uint64_t t = 0;
+      if (more && next(s, t)) {
+        cur = tile_base(t);
+        issue(cur);
+      } else {
+        more = false;
+      }
+      if (s > 0) {
+        run(xf, xb);
+        store(xf, xb, prev);
+      }
+      if (!more) break;
     }
   } else {
     static_assert(TWO && NE == 2, "k_rw prefetch: two-state tiles (32 chunks in a[0:127])");
