@@ -28,6 +28,10 @@
 
 namespace qdc {
 
+#ifndef QDC_RQ_GSPLIT
+#define QDC_RQ_GSPLIT 0
+#endif
+
 constexpr int RQ_R = 16;  // amplitudes per thread per state
 constexpr uint32_t FK_RELAYOUT = 7;
 constexpr int RQ_NT_ONE = 256;  // threads per one-state tile: 2^12 amplitudes = TILE_CHUNKS_1
@@ -77,25 +81,34 @@ __device__ __forceinline__ void rq_q2(cx (&f)[R], cx (&b)[R], const cx* __restri
                                       bool gamma, real* acc_out) {
   cx A[16], B[16];
   if (TWO && gamma) {
-    cx acc[16];
+    // QDC_RQ_GSPLIT: Gamma in two halves of rows (p = 0, 1 then 2, 3), each reduced on its own:
+    // 16 accumulator VGPRs live instead of 32 at the same reduce-scatter cost (two 16-value
+    // reductions ~ one of 32), for register pressure at the 256-VGPR limit
+    constexpr int NH = (QDC_RQ_GSPLIT && R >= 32) ? 2 : 1;
 #pragma unroll
-    for (int k = 0; k < R / 4; ++k) {
-      const int base = rq_base<S1, S2>(k);
+    for (int h = 0; h < NH; ++h) {
+      constexpr int PR = 4 / NH;  // rows per half
+      cx acc[4 * PR];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int k = 0; k < R / 4; ++k) {
+        const int base = rq_base<S1, S2>(k);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const cx bp = b[rq_el<S1, S2>(base, p)], fq = f[rq_el<S1, S2>(base, q)];
-          acc[p * 4 + q] = k == 0 ? vcmul(bp, fq) : vcfma(bp, fq, acc[p * 4 + q]);
-        }
+        for (int pp = 0; pp < PR; ++pp)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int p = h * PR + pp;
+            const cx bp = b[rq_el<S1, S2>(base, p)], fq = f[rq_el<S1, S2>(base, q)];
+            acc[pp * 4 + q] = k == 0 ? vcmul(bp, fq) : vcfma(bp, fq, acc[pp * 4 + q]);
+          }
+      }
+      real v[8 * PR];
+#pragma unroll
+      for (int i = 0; i < 4 * PR; ++i) {
+        v[2 * i] = acc[i].x;
+        v[2 * i + 1] = acc[i].y;
+      }
+      wave_reduce_add<8 * PR>(v, acc_out + h * 8 * PR);
     }
-    real v[32];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      v[2 * i] = acc[i].x;
-      v[2 * i + 1] = acc[i].y;
-    }
-    wave_reduce_add<32>(v, acc_out);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) A[i] = M[i];
@@ -673,6 +686,11 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #ifndef QDC_RW_WAVES
 #define QDC_RW_WAVES 2
 #endif
+// one-state passes without prefetch (the f64 forward by default): 16 amplitudes per lane in f64
+// need ~135 VGPRs, which 2 waves/SIMD would leave half idle
+#ifndef QDC_RW_WAVES_ONE
+#define QDC_RW_WAVES_ONE 2
+#endif
 // S5: five-slot layouts (NE = 2, W = 1): the register-group bit is register slot 4, which
 // stages address like the other four, so covers hold 5 qubits (fewer relayouts); the layout
 // descriptor then spans all 32 registers (rp[16 e + j], chunk offsets offi[8 e + i]).
@@ -682,7 +700,9 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 // four-wave barriers), and the next tile's 16 chunks per lane prefetched into pinned VGPRs as in
 // k_rq (rq_ld / rq_vmwait_two), with a dynamic tail taken block-wide.
 template <bool TWO, int NE, bool PF, int W, bool S5 = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu((PF && TWO) ? 1 : QDC_RW_WAVES, (PF && TWO) ? 1 : QDC_RW_WAVES)))
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(
+    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES,
+    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES)))
 void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
           const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
           uint64_t slot_stride) {
