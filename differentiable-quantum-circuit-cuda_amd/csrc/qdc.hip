@@ -5,6 +5,22 @@
 // (include/qdc/circuit.h).  Everything else has hidden visibility.
 #include "qdc_circuit.hpp"
 #include "qdc_primitives.hpp"
+#ifndef QDC_F64
+#include "qdc_spec.hpp"
+
+// Build-time check of the specialized pass template (qdc_spec.hpp): the runtime compiles its
+// instances on the GPU box from these same headers; this one (an empty program) is never run.
+namespace {
+struct SpecCheckProg {
+  __device__ __forceinline__ void operator()(qdc::cx (&)[32], qdc::cx (&)[32], const qdc::SpecEnv&) const {}
+};
+}  // namespace
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spec_check(
+    qdc::chunk* f, qdc::chunk* b, const qdc::fop* ops, const qdc::cx* mats, qdc::fgeo fg, uint32_t l0,
+    qdc::cx* partials, uint64_t slot_stride) {
+  qdc::rw_spec_two<SpecCheckProg>(f, b, ops, mats, fg, l0, partials, slot_stride);
+}
+#endif
 
 struct qdc_circuit {
   qdc::Circuit impl;
@@ -449,6 +465,51 @@ QDC_API int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1,
                           p.tg.t1, p.tg.t2, (unsigned)(cnt & 0xffffffffu), (unsigned)(cnt >> 32)};
   for (int i = 0; i < 10; ++i) out[i] = v[i];
   return 0;
+}
+
+// Host-only test hook of the specialized reverse passes (qdc_jit.hpp): plan a five-slot
+// two-state pass over n stages (as qdc_rq_plan; every stage a Gamma stage), write its kernel
+// source and compile it with hipcc for gfx950 (not loaded).  name_out receives the kernel name
+// and, after a NUL, the code object's path.  Returns nullptr or an error message.
+QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+                                      const unsigned* t2, const unsigned long long* deps, size_t n,
+                                      char* name_out, size_t cap) {
+#ifdef QDC_F64
+  (void)tile_bits; (void)kinds; (void)t1; (void)t2; (void)deps; (void)n; (void)name_out; (void)cap;
+  return "specialized passes are f32";
+#else
+  if (n == 0 || n > 64 || !name_out || cap < 128) return "invalid arguments";
+  std::vector<qdc::RqStage> st(n);
+  for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, 5);
+  std::vector<qdc::SpecStep> sst;
+  qdc::RqLayout cur = plan.load;
+  for (const qdc::RqStep& s : plan.steps) {
+    qdc::fop F{};
+    if (s.relayout) {
+      F.kind = qdc::FK_RELAYOUT;
+      sst.push_back(qdc::SpecStep{true, cur, s.L, F});
+      cur = s.L;
+      continue;
+    }
+    F.kind = st[s.stage].kind | qdc::FOP_GAMMA;
+    F.t1 = s.cs;
+    const uint32_t kd = st[s.stage].kind;
+    if ((kd == qdc::FK_Q2 || kd == qdc::FK_DIAG) && (s.cs >> 3) > (s.cs & 7u))
+      F.t1 = (s.cs & 7u) * 8u + (s.cs >> 3);  // the runtime's canonical S1 < S2
+    sst.push_back(qdc::SpecStep{false, cur, cur, F});
+  }
+  const std::string body = qdc::spec_program_source(sst, tile_bits);
+  char nm[40];
+  snprintf(nm, sizeof nm, "qdc_spec_%016llx", (unsigned long long)qdc::spec_hash(body));
+  const std::string name = nm, src = qdc::spec_kernel_source(name, body);
+  if (const char* e = qdc::SpecJit::get().compile_only({name}, {src})) return e;
+  const std::string obj = qdc::SpecJit::get().code_object(name);
+  if (name.size() + obj.size() + 2 > cap) return "name buffer too small";
+  std::memcpy(name_out, name.c_str(), name.size() + 1);
+  std::memcpy(name_out + name.size() + 1, obj.c_str(), obj.size() + 1);
+  return nullptr;
+#endif
 }
 
 QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds,

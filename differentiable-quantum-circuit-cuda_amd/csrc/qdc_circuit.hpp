@@ -20,6 +20,7 @@
 #include "qdc_shard.hpp"
 #include "qdc_stage.hpp"
 #include "qdc_fusion.hpp"
+#include "qdc_jit.hpp"
 
 namespace qdc {
 
@@ -239,6 +240,12 @@ struct Circuit {
   // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
   // XCD-aware block order (QDC_RQ_ORDER)
   int rq_order = 0;
+  // reverse passes as straight-line kernels specialized per pass program (qdc_spec.hpp,
+  // qdc_jit.hpp; QDC_SPEC): 0 off, 1 for states of >= spec_min_qubits local qubits, 2 always;
+  // a call whose reverse program needs more than spec_max distinct kernels runs generic
+  int spec_mode = 1;
+  uint32_t spec_min_qubits = 22;
+  uint32_t spec_max = 160;
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
@@ -310,6 +317,9 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
+    if (const char* e = getenv("QDC_SPEC")) spec_mode = atoi(e);
+    if (const char* e = getenv("QDC_SPEC_MIN_QUBITS")) spec_min_qubits = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_SPEC_MAX")) spec_max = (uint32_t)atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -610,6 +620,9 @@ struct Circuit {
     bool s5 = false;   // rq with five register slots (k_rw<true, 2, false, 1, true>)
     uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
     uint32_t tbits = 0;  // amplitude bits of the tile
+    // specialized kernel of a five-slot reverse pass (qdc_jit.hpp): name, source, function
+    std::string spec_name, spec_src;
+    hipFunction_t spec_fn = nullptr;
   };
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
   static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
@@ -960,6 +973,12 @@ struct Circuit {
       }
       uint32_t n = 0;
       it.grad_slots.clear();  // the kernel reduces Gamma stages in execution order
+      const bool spec = spec_wanted() && two && it.s5;
+      std::vector<SpecStep> sst;
+      RqLayout lcur = P.load;
+      it.spec_name.clear();
+      it.spec_src.clear();
+      it.spec_fn = nullptr;
       for (const RqStep& step : P.steps) {
         if (!step.relayout && pslot[step.stage] >= 0)
           it.grad_slots.push_back((uint32_t)pslot[step.stage]);
@@ -967,6 +986,8 @@ struct Circuit {
         if (step.relayout) {
           F.kind = FK_RELAYOUT;
           F.mat = put_layout(step.L);
+          if (spec) sst.push_back(SpecStep{true, lcur, step.L, F});
+          lcur = step.L;
         } else {
           F = pf[step.stage];
           F.t1 = step.cs;
@@ -991,10 +1012,18 @@ struct Circuit {
                 if (sp.slot == (uint32_t)pslot[step.stage]) sp.swapped = true;
           }
         }
+        if (spec && !step.relayout) sst.push_back(SpecStep{false, lcur, lcur, F});
         fops[fo++] = F;
         ++n;
       }
       it.nstage = n;
+      if (spec) {
+        const std::string body = spec_program_source(sst, it.tbits);
+        char nm[40];
+        snprintf(nm, sizeof nm, "qdc_spec_%016llx", (unsigned long long)spec_hash(body));
+        it.spec_name = nm;
+        it.spec_src = spec_kernel_source(it.spec_name, body);
+      }
       if (rq_stats) fprintf(stderr, "rq pass: %zu stages, %u ops (T=%u lc=%u)\n", pf.size(), n, it.tbits, it.lc);
       if (rq_stats >= 2) {  // the pass's stages for offline planner studies (tools/)
         fprintf(stderr, "rq stages %s T=%u perm=%d:", two ? "two" : "one", it.tbits, perm ? 1 : 0);
@@ -1008,6 +1037,36 @@ struct Circuit {
       QDC_HIP(hipMemcpyAsync(d->prog_dev, prog_host, mats_off + mo * sizeof(cx),
                              hipMemcpyHostToDevice, d->ctx.stream));
     }
+    QDC_TRY(spec_load(items));
+    return nullptr;
+  }
+  // specialized reverse passes: single-device, unsharded f32 circuits of >= spec_min_qubits
+  bool spec_wanted() const {
+    return sizeof(real) == 4 && spec_mode > 0 && g == 0 && sh.size() == 1 && rq5() &&
+           (spec_mode >= 2 || nl >= spec_min_qubits);
+  }
+  // compile / load the kernels of this program's specialized passes (none when there are more
+  // distinct ones than spec_max: deep random circuits would compile for minutes)
+  const char* spec_load(std::vector<Item>& items) {
+    std::vector<std::string> names, srcs;
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < items.size(); ++i) {
+      if (items[i].spec_name.empty()) continue;
+      bool seen = false;
+      for (const auto& nm : names) seen = seen || nm == items[i].spec_name;
+      if (!seen) {
+        names.push_back(items[i].spec_name);
+        srcs.push_back(items[i].spec_src);
+      }
+      idx.push_back(i);
+    }
+    if (names.empty() || names.size() > spec_max) return nullptr;
+    QDC_TRY(sh[0].c().use());
+    std::vector<hipFunction_t> fns;
+    SpecJit::get().ensure(sh[0].c().device, names, srcs, fns);
+    for (size_t i : idx)
+      for (size_t k = 0; k < names.size(); ++k)
+        if (names[k] == items[i].spec_name) items[i].spec_fn = fns[k];
     return nullptr;
   }
 
@@ -1041,7 +1100,8 @@ struct Circuit {
   // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
   const char* launch_rq(Ctx& ctx, const char* name, double bytes, const fgeo& fg, bool two,
                         uint32_t tbits, uint32_t l0, chunk* f, chunk* b, const fop* fops,
-                        const cx* mats, cx* partials, uint64_t stride, bool s5) {
+                        const cx* mats, cx* partials, uint64_t stride, bool s5,
+                        hipFunction_t spec = nullptr) {
 #ifndef QDC_F64
     const uint32_t nt = (1u << tbits) / (uint32_t)RQ_R;
     if (!two && s5 && nt == 256) {  // two waves per 2^12 tile, five slots, prefetching
@@ -1088,6 +1148,9 @@ struct Circuit {
       if (two && pfw)
         return ctx.launch_block(name, bytes, k_rw<true, 2, true, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
+      if (two && s5 && spec)  // the pass's straight-line kernel (same resources and grid)
+        return ctx.launch_module(name, bytes, spec, grid, bs, f, b, fops, mats, g, l0, partials,
+                                 stride);
       if (two && s5)
         return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1, true>, grid, bs, f, b, fops,
                                 mats, g, l0, partials, stride);
@@ -1233,7 +1296,7 @@ struct Circuit {
       ctx.next_flops = flops;
       if (it.rq) {
         QDC_TRY(launch_rq(ctx, name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride,
-                          it.s5));
+                          it.s5, it.spec_fn));
       } else if (two) {
         if (it.writes_f)
           QDC_TRY((launch_fused<true, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));

@@ -301,6 +301,30 @@ struct Ctx {
     return nullptr;
   }
 
+  // a kernel from a loaded code object (qdc_jit.hpp), arguments as for launch_block
+  template <typename... Args>
+  const char* launch_module(const char* name, double bytes, hipFunction_t fn, uint32_t grid,
+                            uint32_t block, Args... args) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (prof.on) {
+      a = prof.get();
+      b = prof.get();
+      if (a) (void)hipEventRecord(a, stream);
+    }
+    void* params[] = {(void*)&args...};
+    hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, stream, params, nullptr);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess)
+      return fail("HIP ERROR: launch of kernel %s (specialized) failed with %s.", name,
+                  hipGetErrorName(e));
+    if (prof.on && a && b) {
+      (void)hipEventRecord(b, stream);
+      prof.recs.push_back({name, bytes, next_flops, a, b});
+    }
+    next_flops = 0;
+    return nullptr;
+  }
+
   // --- reduction slots -----------------------------------------------------------------
   // A reduction kernel writes its per-block partials into the next free slot; the slot is
   // later summed into base[dst*RED .. +RED) by k_finalize.  All pending slots share one base.

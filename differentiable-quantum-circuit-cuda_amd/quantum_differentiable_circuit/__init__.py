@@ -388,6 +388,26 @@ def rq_plan(tile_bits, stages, deps=None, precision=None, slots=4):
     return rows[0][3:3 + slots], steps, rows[-1][3:3 + slots]
 
 
+def spec_selftest(tile_bits, stages, deps=None):
+    """Compile the specialized reverse-pass kernel of a five-slot two-state f32 pass (host only:
+    the runtime's generator and hipcc, qdc_spec_selftest).  stages as for rq_plan.  Returns
+    (kernel name, code object path); raises RuntimeError with the runtime's message."""
+    lib = load("f32")
+    n = len(stages)
+    kinds = (C.c_uint * n)(*[int(s[0]) for s in stages])
+    t1 = (C.c_uint * n)(*[int(s[1]) for s in stages])
+    t2 = (C.c_uint * n)(*[int(s[2]) for s in stages])
+    dp = (C.c_ulonglong * n)(*[int(d) for d in (deps or [0] * n)])
+    out = C.create_string_buffer(1024)
+    err = lib.qdc_spec_selftest(tile_bits, kinds, t1, t2, dp, n, out, 1024)
+    if err:
+        raise RuntimeError(err.decode())
+    raw = out.raw
+    name = raw.split(b"\0", 1)[0].decode()
+    path = raw[len(name) + 1:].split(b"\0", 1)[0].decode()
+    return name, path
+
+
 # ---------------------------------------------------------------------------------------
 # QuantizedTensor (src/quantized_tensor.rs:54-238) over the 18-function C ABI
 # ---------------------------------------------------------------------------------------

@@ -209,6 +209,15 @@ size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds, co
                    const unsigned* t2, const unsigned long long* deps, size_t n,
                    unsigned* steps, size_t cap);
 
+/* Test hook (host only): the specialized reverse-pass kernel of a five-slot two-state pass over
+ * n stages (kinds / t1 / t2 / deps as qdc_rq_plan, every stage accumulating Gamma): the
+ * runtime's source generator and hipcc for gfx950, as a circuit call on a GPU box runs them
+ * (qdc_jit.hpp), without loading the code object.  name_out (cap >= 128) receives the kernel
+ * name, a NUL, then the code object's path.  Returns NULL, or an error message. */
+const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+                              const unsigned* t2, const unsigned long long* deps, size_t n,
+                              char* name_out, size_t cap);
+
 /* Test hook (host only): the launch geometry a single-gate op gets (qdc_device.hpp plan_gate)
  * on an n-qubit state: R = 2 (one-qubit, pos2 == pos1) or 4; two_states: the op reads both
  * states (tile of 2^9 chunks, else 2^10); far_tile: targets beyond chunk bit 5 go to the tile

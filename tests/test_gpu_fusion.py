@@ -320,3 +320,35 @@ def test_dynamic_tail_is_deterministic(prec):
     tol = 1e-5 if prec == "f32" else 1e-12
     assert F.normrel(g3, g1) <= tol and F.normrel(d3, d1) <= tol
     print(f"[dyn] {prec} n={n}: static-only vs dynamic tail, grads {F.normrel(g3, g1):.2e}")
+
+
+@pytest.mark.parametrize("case", ["layered14", "random14", "layered18"])
+def test_specialized_reverse_passes_equal_interpreted(case):
+    """Reverse passes compiled per pass program (csrc/qdc_spec.hpp, qdc_jit.hpp: straight-line
+    stages, compile-time slot cases and relayout descriptors; QDC_SPEC=2 forces them at any
+    size, 0 keeps the interpreted k_rw) run the same stage arithmetic in the same order as the
+    interpreted kernel: densities, gradients and both states are bit-identical, and within the
+    floors of the oracle."""
+    import quantum_differentiable_circuit as q
+    kind, n = case[:-2], int(case[-2:])
+    if kind == "layered":
+        ins, var = O.layered_circuit(n, 4, seed=31)
+        const, psi0 = [], None
+    else:
+        ins, const, var = O.random_circuit(n, 160, seed=300 + n, density_every=3)
+        psi0 = O.random_state(np.random.default_rng(n + 1), n)
+    fl = F.Floor("f32", n, ins, const, var, psi0=psi0, run=False)
+    out = {}
+    for mode in ("0", "2"):
+        c = build_env("f32", n, ins, {"QDC_SPEC": mode, "QDC_SPEC_MAX": 400})
+        if psi0 is not None:
+            c.set_state_from_vector(fl.psi0)
+        d = c.forward(fl.const, fl.var)
+        g = c.backward(fl.cots, fl.const, fl.var)
+        out[mode] = (np.concatenate([x.reshape(-1) for x in d]), g, c.get_state(0), c.get_state(2))
+        what = f"{case} spec={mode} "
+        fl.check("grads", g, what)
+        fl.check("uncomputed", out[mode][2], what)
+    for k, name in enumerate(("densities", "grads", "fwd", "bwd")):
+        assert np.array_equal(out["0"][k], out["2"][k]), f"{case}: specialized {name} differ"
+    print(f"[spec] {case}: specialized reverse passes bit-identical to the interpreted kernel")
