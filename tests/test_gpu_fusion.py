@@ -345,10 +345,12 @@ def test_specialized_reverse_passes_equal_interpreted(case):
             c.set_state_from_vector(fl.psi0)
         d = c.forward(fl.const, fl.var)
         g = c.backward(fl.cots, fl.const, fl.var)
-        out[mode] = (np.concatenate([x.reshape(-1) for x in d]), g, c.get_state(0), c.get_state(2))
+        flat = lambda xs: np.concatenate([np.asarray(x).reshape(-1) for x in xs])
+        out[mode] = (flat(d), flat(g), np.asarray(c.get_state(0)), np.asarray(c.get_state(2)))
         what = f"{case} spec={mode} "
         fl.check("grads", g, what)
         fl.check("uncomputed", out[mode][2], what)
+    # (grads are per-gate arrays of different shapes: compared flattened)
     for k, name in enumerate(("densities", "grads", "fwd", "bwd")):
         assert np.array_equal(out["0"][k], out["2"][k]), f"{case}: specialized {name} differ"
     print(f"[spec] {case}: specialized reverse passes bit-identical to the interpreted kernel")
