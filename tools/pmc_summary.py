@@ -38,6 +38,8 @@ def bench_name(kernel):
         two, wf = m.group(1) == "true", m.group(3) == "true"
         return ("fused_reverse" if wf else "fused_inject") if two else \
                ("fused_apply" if wf else "fused_density")
+    if kernel.startswith("qdc_spec_"):  # a specialized reverse pass (csrc/qdc_spec.hpp)
+        return "fused_reverse"
     m = re.search(r"k_r[qw]<(true|false), \d+[^>]*>", kernel)
     if m:  # register-resident gate passes (qdc_rq.hpp): k_rq<TWO, NT, PF>, k_rw<TWO, NE, PF>
         return "fused_reverse" if m.group(1) == "true" else "fused_apply"
