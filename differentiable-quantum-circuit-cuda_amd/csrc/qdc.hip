@@ -5,22 +5,42 @@
 // (include/qdc/circuit.h).  Everything else has hidden visibility.
 #include "qdc_circuit.hpp"
 #include "qdc_primitives.hpp"
-#ifndef QDC_F64
 #include "qdc_spec.hpp"
 
-// Build-time check of the specialized pass template (qdc_spec.hpp): the runtime compiles its
-// instances on the GPU box from these same headers; this one (an empty program) is never run.
+// Build-time check of the specialized pass templates (qdc_spec.hpp): the runtime compiles their
+// instances on the GPU box from these same headers; these (one exchange of each form) never run.
 namespace {
-struct SpecCheckProg {
-  __device__ __forceinline__ void operator()(qdc::cx (&)[32], qdc::cx (&)[32], const qdc::SpecEnv&) const {}
+template <int R>
+struct SpecCheckTwo {
+  __device__ __forceinline__ void operator()(qdc::cx (&xf)[R], qdc::cx (&xb)[R], const qdc::SpecEnv& E) const {
+    constexpr uint32_t z[32] = {};
+    qdc::spec_xchg_imm<6, false>(xf, E, z, z);
+    qdc::spec_xchg<6, false>(xb, E, z, z, z, z);
+  }
+};
+template <int R, int TB>
+struct SpecCheckOne {
+  __device__ __forceinline__ void operator()(qdc::cx (&x)[R], const qdc::SpecEnv& E) const {
+    constexpr uint32_t z[32] = {};
+    qdc::spec_xchg_imm<TB, true>(x, E, z, z);
+    qdc::spec_xchg<TB, true>(x, E, z, z, z, z);
+  }
 };
 }  // namespace
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spec_check(
-    qdc::chunk* f, qdc::chunk* b, const qdc::fop* ops, const qdc::cx* mats, qdc::fgeo fg, uint32_t l0,
-    qdc::cx* partials, uint64_t slot_stride) {
-  qdc::rw_spec_two<SpecCheckProg>(f, b, ops, mats, fg, l0, partials, slot_stride);
-}
+#define QDC_SPEC_CHECK(name, threads, pass)                                                       \
+  __global__ __launch_bounds__(threads) void name(qdc::chunk* f, qdc::chunk* b, const qdc::fop* ops, \
+                                                  const qdc::cx* mats, qdc::fgeo fg, uint32_t l0,    \
+                                                  qdc::cx* partials, uint64_t slot_stride) {         \
+    pass(f, b, ops, mats, fg, l0, partials, slot_stride);                                        \
+  }
+#ifndef QDC_F64
+QDC_SPEC_CHECK(k_spec_check_two, 64, (qdc::rw_pass<true, 2, false, 1, true, SpecCheckTwo<32>>))
+QDC_SPEC_CHECK(k_spec_check_one, 256, (qdc::rq_pass<false, 256, true, SpecCheckOne<16, 8>>))
+#else
+QDC_SPEC_CHECK(k_spec_check_two, 64, (qdc::rw_pass<true, 1, false, 1, false, SpecCheckTwo<16>>))
+QDC_SPEC_CHECK(k_spec_check_one, 128, (qdc::rw_pass<false, 1, false, 2, false, SpecCheckOne<16, 7>>))
 #endif
+#undef QDC_SPEC_CHECK
 
 struct qdc_circuit {
   qdc::Circuit impl;
@@ -467,21 +487,22 @@ QDC_API int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1,
   return 0;
 }
 
-// Host-only test hook of the specialized reverse passes (qdc_jit.hpp): plan a five-slot
-// two-state pass over n stages (as qdc_rq_plan; every stage a Gamma stage), write its kernel
-// source and compile it with hipcc for gfx950 (not loaded).  name_out receives the kernel name
+// Host-only test hook of the specialized passes (qdc_jit.hpp): plan a pass over n stages (as
+// qdc_rq_plan; a two-state pass's stages all Gamma stages) on the runtime's tile of the
+// precision, write its kernel source and compile it with hipcc for gfx950 (not loaded).  name_out receives the kernel name
 // and, after a NUL, the code object's path.  Returns nullptr or an error message.
 QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
                                       const unsigned* t2, const unsigned long long* deps, size_t n,
                                       char* name_out, size_t cap) {
-#ifdef QDC_F64
-  (void)tile_bits; (void)kinds; (void)t1; (void)t2; (void)deps; (void)n; (void)name_out; (void)cap;
-  return "specialized passes are f32";
-#else
   if (n == 0 || n > 64 || !name_out || cap < 128) return "invalid arguments";
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
-  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, 5);
+  // the runtime's tiles: f32 11 two-state (five slots), 12 one-state; f64 10 two-state, 11 one-state
+  const unsigned t2bits = sizeof(qdc::real) == 4 ? 11u : 10u;
+  if (tile_bits != t2bits && tile_bits != t2bits + 1) return "tile_bits: not a specialized pass's tile";
+  const bool two = tile_bits == t2bits;
+  const qdc::SpecKind K = two ? qdc::spec_kind_two() : qdc::spec_kind_one(tile_bits);
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, K.ns);
   std::vector<qdc::SpecStep> sst;
   qdc::RqLayout cur = plan.load;
   for (const qdc::RqStep& s : plan.steps) {
@@ -492,24 +513,21 @@ QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds,
       cur = s.L;
       continue;
     }
-    F.kind = st[s.stage].kind | qdc::FOP_GAMMA;
+    F.kind = st[s.stage].kind | (two ? qdc::FOP_GAMMA : 0u);
     F.t1 = s.cs;
     const uint32_t kd = st[s.stage].kind;
     if ((kd == qdc::FK_Q2 || kd == qdc::FK_DIAG) && (s.cs >> 3) > (s.cs & 7u))
       F.t1 = (s.cs & 7u) * 8u + (s.cs >> 3);  // the runtime's canonical S1 < S2
     sst.push_back(qdc::SpecStep{false, cur, cur, F});
   }
-  const std::string body = qdc::spec_program_source(sst, tile_bits);
-  char nm[40];
-  snprintf(nm, sizeof nm, "qdc_spec_%016llx", (unsigned long long)qdc::spec_hash(body));
-  const std::string name = nm, src = qdc::spec_kernel_source(name, body);
+  const std::string body = qdc::spec_program_source(sst, tile_bits, K);
+  const std::string name = qdc::spec_kernel_name(body, K), src = qdc::spec_kernel_source(name, body, K);
   if (const char* e = qdc::SpecJit::get().compile_only({name}, {src})) return e;
   const std::string obj = qdc::SpecJit::get().code_object(name);
   if (name.size() + obj.size() + 2 > cap) return "name buffer too small";
   std::memcpy(name_out, name.c_str(), name.size() + 1);
   std::memcpy(name_out + name.size() + 1, obj.c_str(), obj.size() + 1);
   return nullptr;
-#endif
 }
 
 QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds,

@@ -240,12 +240,16 @@ struct Circuit {
   // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
   // XCD-aware block order (QDC_RQ_ORDER)
   int rq_order = 0;
-  // reverse passes as straight-line kernels specialized per pass program (qdc_spec.hpp,
-  // qdc_jit.hpp; QDC_SPEC): 0 off, 1 for states of >= spec_min_qubits local qubits, 2 always;
-  // a call whose reverse program needs more than spec_max distinct kernels runs generic
+  // register-resident passes as straight-line kernels specialized per pass program
+  // (qdc_spec.hpp, qdc_jit.hpp; QDC_SPEC): 0 off, 1 for states of >= spec_min_qubits local
+  // qubits, 2 always; a call whose program needs more than spec_max distinct kernels runs generic
   int spec_mode = 1;
   uint32_t spec_min_qubits = 22;
   uint32_t spec_max = 160;
+  int spec_fwd = 1;  // forward (one-state) passes too (QDC_SPEC_FWD)
+  // generated kernels by pass program (key: qdc_circuit build_program), with their functions
+  std::map<std::vector<uint32_t>, SpecEntry> spec_cache;
+  uint64_t spec_epoch = 0;
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
@@ -320,6 +324,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_SPEC")) spec_mode = atoi(e);
     if (const char* e = getenv("QDC_SPEC_MIN_QUBITS")) spec_min_qubits = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_MAX")) spec_max = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_SPEC_FWD")) spec_fwd = atoi(e);
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -620,8 +625,8 @@ struct Circuit {
     bool s5 = false;   // rq with five register slots (k_rw<true, 2, false, 1, true>)
     uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
     uint32_t tbits = 0;  // amplitude bits of the tile
-    // specialized kernel of a five-slot reverse pass (qdc_jit.hpp): name, source, function
-    std::string spec_name, spec_src;
+    // specialized kernel of a five-slot reverse pass or a one-state forward pass (qdc_jit.hpp): name, source, function
+    SpecEntry* spec = nullptr;  // specialized kernel of the pass (qdc_jit.hpp), or none
     hipFunction_t spec_fn = nullptr;
   };
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
@@ -699,6 +704,7 @@ struct Circuit {
                             const std::vector<uint32_t>& var_idx, uint32_t nvar,
                             const std::vector<uint32_t>& out_idx, const Flat* dg) {
     stage_post.clear();
+    if (spec_cache.size() >= 4096) spec_cache.clear();  // bounded; items of this call point into it
     std::vector<std::vector<std::vector<uint32_t>>> stages_of(items.size());
     size_t nops = 0;
     for (size_t ii = 0; ii < items.size(); ++ii)
@@ -973,11 +979,16 @@ struct Circuit {
       }
       uint32_t n = 0;
       it.grad_slots.clear();  // the kernel reduces Gamma stages in execution order
-      const bool spec = spec_wanted() && two && it.s5;
+      // the kernels launch_rq runs: f32 two-state five-slot k_rw, one-state prefetching k_rq on
+      // 2^12 tiles; f64 two-state k_rw on 2^10 tiles, one-state on 2^10 / 2^11
+      const bool f32 = sizeof(real) == 4;
+      const bool spec1 = spec_on() && spec_fwd && !two &&
+                         (f32 ? (!it.s5 && it.tbits == 12 && rq_prefetch && !(rq_wave & 2))
+                              : (it.tbits == 10 || it.tbits == 11));
+      const bool spec = spec1 || (spec_on() && two && (f32 ? (it.s5 && rq5()) : it.tbits == 10));
       std::vector<SpecStep> sst;
       RqLayout lcur = P.load;
-      it.spec_name.clear();
-      it.spec_src.clear();
+      it.spec = nullptr;
       it.spec_fn = nullptr;
       for (const RqStep& step : P.steps) {
         if (!step.relayout && pslot[step.stage] >= 0)
@@ -1018,11 +1029,34 @@ struct Circuit {
       }
       it.nstage = n;
       if (spec) {
-        const std::string body = spec_program_source(sst, it.tbits);
-        char nm[40];
-        snprintf(nm, sizeof nm, "qdc_spec_%016llx", (unsigned long long)spec_hash(body));
-        it.spec_name = nm;
-        it.spec_src = spec_kernel_source(it.spec_name, body);
+        // the source is generated once per distinct program (per process): the key is
+        // everything it depends on, the layouts, stage kinds, slot cases and Γ flags
+        std::vector<uint32_t> key = {spec1 ? 1u : 2u, it.tbits, spec_imm() ? 1u : 0u};
+        auto put_layout_key = [&](const RqLayout& L) {
+          key.push_back(L.ns | (L.tfix ? 0x100u : 0u));
+          for (uint32_t q = 0; q < RQ_SLOTS_MAX; ++q) key.push_back(L.slot[q]);
+          for (int q = 0; q < 3; ++q) key.push_back(L.tfirst[q]);
+        };
+        put_layout_key(P.load);
+        for (const SpecStep& ss : sst) {
+          if (ss.relayout) {
+            key.push_back(0xffffffffu);
+            put_layout_key(ss.Ln);
+          } else {
+            key.push_back(ss.F.kind);
+            key.push_back(ss.F.t1);
+          }
+        }
+        auto hit = spec_cache.find(key);
+        if (hit == spec_cache.end()) {
+          const SpecKind K = spec1 ? spec_kind_one(it.tbits) : spec_kind_two();
+          const std::string body = spec_program_source(sst, it.tbits, K);
+          SpecEntry e;
+          e.name = spec_kernel_name(body, K);
+          e.src = spec_kernel_source(e.name, body, K);
+          hit = spec_cache.emplace(std::move(key), std::move(e)).first;
+        }
+        it.spec = &hit->second;
       }
       if (rq_stats) fprintf(stderr, "rq pass: %zu stages, %u ops (T=%u lc=%u)\n", pf.size(), n, it.tbits, it.lc);
       if (rq_stats >= 2) {  // the pass's stages for offline planner studies (tools/)
@@ -1040,36 +1074,46 @@ struct Circuit {
     QDC_TRY(spec_load(items));
     return nullptr;
   }
-  // specialized reverse passes: single-device, unsharded f32 circuits of >= spec_min_qubits
-  bool spec_wanted() const {
-    return sizeof(real) == 4 && spec_mode > 0 && g == 0 && sh.size() == 1 && rq5() &&
-           (spec_mode >= 2 || nl >= spec_min_qubits);
+  // specialized passes: single-device, unsharded circuits of >= spec_min_qubits local qubits
+  bool spec_on() const {
+    return spec_mode > 0 && g == 0 && sh.size() == 1 && (spec_mode >= 2 || nl >= spec_min_qubits);
   }
   // compile / load the kernels of this program's specialized passes (none when there are more
   // distinct ones than spec_max: deep random circuits would compile for minutes)
   const char* spec_load(std::vector<Item>& items) {
-    std::vector<std::string> names, srcs;
-    std::vector<size_t> idx;
-    for (size_t i = 0; i < items.size(); ++i) {
-      if (items[i].spec_name.empty()) continue;
-      bool seen = false;
-      for (const auto& nm : names) seen = seen || nm == items[i].spec_name;
-      if (!seen) {
-        names.push_back(items[i].spec_name);
-        srcs.push_back(items[i].spec_src);
+    if (items.empty()) return nullptr;
+    const int dev = sh[0].c().device;
+    std::vector<SpecEntry*> todo;  // distinct kernels of this call not loaded on dev yet
+    size_t distinct = 0;
+    ++spec_epoch;
+    for (Item& it : items) {
+      if (!it.spec) continue;
+      if (it.spec->epoch != spec_epoch) {
+        it.spec->epoch = spec_epoch;
+        ++distinct;
+        if (!it.spec->fn.count(dev)) todo.push_back(it.spec);
       }
-      idx.push_back(i);
     }
-    if (names.empty() || names.size() > spec_max) return nullptr;
-    QDC_TRY(sh[0].c().use());
-    std::vector<hipFunction_t> fns;
-    SpecJit::get().ensure(sh[0].c().device, names, srcs, fns);
-    for (size_t i : idx)
-      for (size_t k = 0; k < names.size(); ++k)
-        if (names[k] == items[i].spec_name) items[i].spec_fn = fns[k];
+    if (distinct == 0 || distinct > spec_max) return nullptr;
+    if (!todo.empty()) {
+      std::vector<std::string> names, srcs;
+      for (const SpecEntry* e : todo) {
+        names.push_back(e->name);
+        srcs.push_back(e->src);
+      }
+      QDC_TRY(sh[0].c().use());
+      std::vector<hipFunction_t> fns;
+      SpecJit::get().ensure(dev, names, srcs, fns);
+      for (size_t k = 0; k < todo.size(); ++k)
+        if (fns[k]) todo[k]->fn[dev] = fns[k];
+    }
+    for (Item& it : items) {
+      if (!it.spec) continue;
+      auto f = it.spec->fn.find(dev);
+      it.spec_fn = f == it.spec->fn.end() ? nullptr : f->second;
+    }
     return nullptr;
   }
-
   // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
   // gradient gates write partials for gradient buffer rows var_idx[...].
   template <bool TWO, bool HASRED, bool WF, int NT>
@@ -1188,6 +1232,8 @@ struct Circuit {
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
     last_fused_ndyn = 0;
+    if (!two && nt == 256 && pf && spec)  // the pass's straight-line kernel (same resources and grid)
+      return ctx.launch_module(name, bytes, spec, grid, nt, f, b, fops, mats, g, l0, partials, stride);
 #define QDC_RQ_LAUNCH(T, N, P)                                                            \
   if (two == T && nt == N && pf == P)                                                     \
     return ctx.launch_block(name, bytes, k_rq<T, N, P>, grid, nt, f, b, fops, mats, g, l0, \
@@ -1225,6 +1271,8 @@ struct Circuit {
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
     last_fused_ndyn = g.ndyn ? ctx.last_ndyn : 0u;
+    if (spec)  // the pass's straight-line kernel (same resources and grid)
+      return ctx.launch_module(name, bytes, spec, grid, bs, f, b, fops, mats, g, l0, partials, stride);
     if (two)
       return ctx.launch_block(name, bytes, k_rw<true, 1, false, 1>, grid, bs, f, b, fops, mats, g, l0,
                               partials, stride);

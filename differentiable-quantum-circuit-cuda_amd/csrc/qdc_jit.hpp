@@ -1,5 +1,6 @@
-// qdc_jit.hpp — the specialized reverse-pass kernels (qdc_spec.hpp): source per pass program,
-// compiled with hipcc for gfx950 on first use, cached on disk and per device.
+// qdc_jit.hpp — the specialized pass kernels (qdc_spec.hpp; two-state reverse passes and
+// one-state forward passes): source per pass program, compiled with hipcc for gfx950 on first
+// use, cached on disk and per device.
 //
 // A pass program becomes a functor of straight-line stage calls; its source text (hashed)
 // names the kernel, so passes with the same program share one kernel, across circuits and
@@ -39,6 +40,14 @@ inline uint64_t spec_hash(const std::string& s) {
   return h;
 }
 
+// relayouts with immediate LDS offsets (spec_xchg_imm; QDC_SPEC_IMM=0: the XOR form)
+inline bool spec_imm() {
+  static const int on = [] {
+    const char* e = getenv("QDC_SPEC_IMM");
+    return e ? atoi(e) : 1;
+  }();
+  return on != 0;
+}
 // Source of one pass program: steps as emitted into the program (relayouts with the layouts
 // before and after, stages with their fop), in order.
 struct SpecStep {
@@ -46,59 +55,143 @@ struct SpecStep {
   RqLayout Lc, Ln;  // relayout: current and new layout
   fop F;            // stage: kind (+ FOP_GAMMA), slot case in t1
 };
-inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint32_t T) {
+// The generic kernel a specialized one replaces, as the generated source names it.
+struct SpecKind {
+  bool two;            // two-state (Gamma stages) or one-state
+  uint32_t tb, ns;     // thread bits and register slots of a tile (registers per state 2^ns)
+  bool bar;            // several waves per tile: block barriers around relayouts
+  const char* prefix;  // kernel name prefix (the bench's kernel classes key on it)
+  const char* pass;    // the generic kernel's body with the program
+  uint32_t threads;
+  const char* waves;   // amdgpu_waves_per_eu of the generic kernel
+};
+#ifndef QDC_F64
+// k_rw<true, 2, false, 1, true>: f32 two-state, one wave, five slots
+inline SpecKind spec_kind_two() {
+  return {true, 6, 5, false, "qdc_spec_", "qdc::rw_pass<true, 2, false, 1, true, Prog>", 64,
+          "QDC_RW_WAVES, QDC_RW_WAVES"};
+}
+// k_rq<false, 256, true>: f32 one-state, four waves, prefetching
+inline SpecKind spec_kind_one(uint32_t) {
+  return {false, 8, 4, true, "qdc_specf_", "qdc::rq_pass<false, 256, true, Prog>", 256,
+          "QDC_RQ_PF_WAVES"};
+}
+#else
+// k_rw<true, 1, false, 1>: f64 two-state, one wave
+inline SpecKind spec_kind_two() {
+  return {true, 6, 4, false, "qdc_spec_d_", "qdc::rw_pass<true, 1, false, 1, false, Prog>", 64,
+          "QDC_RW_WAVES, QDC_RW_WAVES"};
+}
+// k_rw<false, 1, false, W>: f64 one-state, W = 1 (2^10 tiles) or 2 (2^11)
+inline SpecKind spec_kind_one(uint32_t T) {
+  if (T == 10)
+    return {false, 6, 4, false, "qdc_specf_d_", "qdc::rw_pass<false, 1, false, 1, false, Prog>", 64,
+            "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};
+  return {false, 7, 4, true, "qdc_specf_d_", "qdc::rw_pass<false, 1, false, 2, false, Prog>", 128,
+          "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};
+}
+#endif
+inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint32_t T, const SpecKind& K) {
   std::string b;
   char tmp[512];
   uint32_t ri = 0;
-  auto arr = [&](const uint32_t* v, int n) {
+  const uint32_t TB = K.tb, NR = 1u << K.ns;
+  snprintf(tmp, sizeof tmp, "<%u, %s>", TB, K.bar ? "true" : "false");
+  const std::string xt = tmp;
+  auto arr = [&](const uint32_t* v, uint32_t n) {
     std::string s = "{";
-    for (int i = 0; i < n; ++i) {
+    for (uint32_t i = 0; i < n; ++i) {
       snprintf(tmp, sizeof tmp, "%s%uu", i ? "," : "", v[i]);
       s += tmp;
     }
     return s + "}";
   };
+  const std::string nr = std::to_string(NR);
   for (size_t j = 0; j < steps.size(); ++j) {
     const SpecStep& s = steps[j];
+    if (s.relayout && spec_imm()) {
+      // LDS index = bit permutation a(): the current layout's thread bits -> 0..TB-1, slots
+      // -> TB..
+      uint32_t a[32] = {}, thc[8], thn[8];
+      const uint32_t nlc = s.Lc.threads(T, thc);
+      s.Ln.threads(T, thn);
+      for (uint32_t k = 0; k < TB && k < nlc; ++k) a[thc[k]] = k;
+      for (uint32_t q = 0; q < s.Lc.ns; ++q) a[s.Lc.slot[q]] = TB + q;
+      uint32_t pn[8], offr[32];
+      for (uint32_t k = 0; k < TB; ++k) pn[k] = (uint32_t)sizeof(cx) << a[thn[k]];
+      for (uint32_t j = 0; j < NR; ++j) {
+        uint32_t o = 0;
+        for (uint32_t q = 0; q < s.Ln.ns; ++q)
+          if ((j >> q) & 1u) o |= 1u << a[s.Ln.slot[q]];
+        offr[j] = o * (uint32_t)sizeof(cx);
+      }
+      b += "    { constexpr uint32_t pn[" + std::to_string(TB) + "] = " + arr(pn, TB) + ", offr[" + nr +
+           "] = " + arr(offr, NR) + ";\n      ";
+      b += K.two ? "spec_xchg_imm" + xt + "(xf, E, pn, offr); spec_xchg_imm" + xt + "(xb, E, pn, offr); }\n"
+                 : "spec_xchg_imm" + xt + "(x, E, pn, offr); }\n";
+      continue;
+    }
     if (s.relayout) {
       const rq_layout c = rq_descriptor(s.Lc, T), n = rq_descriptor(s.Ln, T);
-      b += "    { constexpr uint32_t rc[32] = " + arr(c.rp, 32) + ", tc[8] = " + arr(c.tv, 8) +
-           ", rn[32] = " + arr(n.rp, 32) + ", tn[8] = " + arr(n.tv, 8) +
-           ";\n      spec_xchg(xf, E, rc, tc, rn, tn); spec_xchg(xb, E, rc, tc, rn, tn); }\n";
+      b += "    { constexpr uint32_t rc[" + nr + "] = " + arr(c.rp, NR) + ", tc[8] = " + arr(c.tv, 8) +
+           ", rn[" + nr + "] = " + arr(n.rp, NR) + ", tn[8] = " + arr(n.tv, 8) + ";\n      ";
+      b += K.two ? "spec_xchg" + xt + "(xf, E, rc, tc, rn, tn); spec_xchg" + xt + "(xb, E, rc, tc, rn, tn); }\n"
+                 : "spec_xchg" + xt + "(x, E, rc, tc, rn, tn); }\n";
       continue;
     }
     const uint32_t kind = s.F.kind & 7u;
-    const bool gamma = (s.F.kind & FOP_GAMMA) != 0;
+    const bool gamma = K.two && (s.F.kind & FOP_GAMMA) != 0;
     const uint32_t c = s.F.t1;
-    if (kind == FK_Q1)
-      snprintf(tmp, sizeof tmp, "    rq_q1<%u, true, 32>(xf, xb, E.mats + E.ops[%zu].mat, %s, &E.accw[%u][0]);\n",
-               c, j, gamma ? "true" : "false", ri);
+    std::string tpl = kind == FK_Q1 ? "rq_q1<" + std::to_string(c)
+                                    : std::string(kind == FK_DIAG ? "rq_diag<" : "rq_q2<") +
+                                          std::to_string(c >> 3) + ", " + std::to_string(c & 7u);
+    if (K.two)
+      snprintf(tmp, sizeof tmp, "    %s, true, %u>(xf, xb, E.mats + E.ops[%zu].mat, %s, &E.accw[%u][0]);\n",
+               tpl.c_str(), NR, j, gamma ? "true" : "false", ri);
     else
-      snprintf(tmp, sizeof tmp, "    %s<%u, %u, true, 32>(xf, xb, E.mats + E.ops[%zu].mat, %s, &E.accw[%u][0]);\n",
-               kind == FK_DIAG ? "rq_diag" : "rq_q2", c >> 3, c & 7u, j, gamma ? "true" : "false", ri);
+      snprintf(tmp, sizeof tmp, "    %s, false, %u>(x, x, E.mats + E.ops[%zu].mat, false, nullptr);\n",
+               tpl.c_str(), NR, j);
     b += tmp;
     if (gamma) ++ri;
   }
   return b;
 }
-inline std::string spec_kernel_source(const std::string& name, const std::string& body) {
+// kernel name (prefix + hash of the generic kernel and the program) and source
+inline std::string spec_kernel_name(const std::string& body, const SpecKind& K) {
+  char nm[48];
+  snprintf(nm, sizeof nm, "%s%016llx", K.prefix,
+           (unsigned long long)spec_hash(std::string(K.pass) + "\n" + body));
+  return nm;
+}
+inline std::string spec_kernel_source(const std::string& name, const std::string& body, const SpecKind& K) {
+  const std::string R = std::to_string(1u << K.ns);
+  const std::string args =
+      K.two ? "qdc::cx (&xf)[" + R + "], qdc::cx (&xb)[" + R + "], const qdc::SpecEnv& E"
+            : "qdc::cx (&x)[" + R + "], const qdc::SpecEnv& E";
   return "#include \"qdc_spec.hpp\"\n"
          "namespace {\n"
          "struct Prog {\n"
-         "  __device__ __forceinline__ void operator()(qdc::cx (&xf)[32], qdc::cx (&xb)[32],\n"
-         "                                             const qdc::SpecEnv& E) const {\n"
+         "  __device__ __forceinline__ void operator()(" + args + ") const {\n"
          "    using namespace qdc;\n" +
          body +
          "  }\n"
          "};\n"
          "}  // namespace\n"
-         "extern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))\n"
+         "extern \"C\" __global__ __launch_bounds__(" + std::to_string(K.threads) +
+         ") __attribute__((amdgpu_waves_per_eu(" + K.waves + ")))\n"
          "void " + name + "(qdc::chunk* __restrict__ f, qdc::chunk* __restrict__ b,\n"
          "    const qdc::fop* __restrict__ ops, const qdc::cx* __restrict__ mats, qdc::fgeo fg,\n"
          "    uint32_t l0, qdc::cx* __restrict__ partials, uint64_t slot_stride) {\n"
-         "  qdc::rw_spec_two<Prog>(f, b, ops, mats, fg, l0, partials, slot_stride);\n"
+         "  " + K.pass + "(f, b, ops, mats, fg, l0, partials, slot_stride);\n"
          "}\n";
 }
+
+// one generated kernel: name, source, and its function per device once loaded
+struct SpecEntry {
+  std::string name, src;
+  std::map<int, hipFunction_t> fn;
+  uint64_t epoch = 0;  // last call (spec_load) that counted it
+};
 
 class SpecJit {
  public:
@@ -171,7 +264,7 @@ class SpecJit {
   }
   std::string obj_path(const std::string& name) const { return dir + "/" + name + ".hsaco"; }
   void disable(const std::string& why) {
-    if (state != -1) fprintf(stderr, "qdc: specialized reverse passes off (%s)\n", why.c_str());
+    if (state != -1) fprintf(stderr, "qdc: specialized passes off (%s)\n", why.c_str());
     state = -1;
   }
   bool init() {
@@ -205,9 +298,13 @@ class SpecJit {
   }
   // the library's own compile-time switches, so the kernels agree with it
   static std::string defines() {
-    char b[256];
-    snprintf(b, sizeof b, "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d", (int)QDC_DYN_TAIL,
-             (int)FMAX_OPS, (int)FMAX_GRAD_RQ);
+    char b[512];
+    snprintf(b, sizeof b,
+             "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
+             "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d%s",
+             (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
+             (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
+             sizeof(real) == 8 ? " -DQDC_F64" : "");
     return b;
   }
   bool compile(const std::vector<std::string>& names, const std::vector<std::string>& srcs,

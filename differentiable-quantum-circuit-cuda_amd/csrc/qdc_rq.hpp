@@ -24,6 +24,8 @@
 // loads/stores go straight between HBM and registers.  Every program ends in L0.
 #pragma once
 
+#include <type_traits>
+
 #include "qdc_kernels.hpp"
 
 namespace qdc {
@@ -426,11 +428,20 @@ __device__ __forceinline__ void rw_vmwait(uint32_t first, vec16 (&v)[32]) {
 #endif
 // PF: software pipeline — the next tile's chunks are loaded into registers while this tile's
 // stages run (2x the state registers, so fewer waves).
-template <bool TWO, int NT, bool PF>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF ? QDC_RQ_PF_WAVES : 4)))
-void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
-          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
-          uint64_t slot_stride) {
+// PROG (not void): the pass program as a functor of straight-line stage calls (qdc_spec.hpp,
+// one-state specialized passes) in place of the interpreted op loop; everything else the same.
+struct SpecEnv {
+  const cx* mats;
+  const fop* ops;
+  real (*accw)[FACC];  // two-state: the Gamma stage accumulators
+  uint32_t t;          // the block's thread
+  char* bufb;          // the relayout buffer
+};
+template <bool TWO, int NT, bool PF, class PROG = void>
+__device__ __forceinline__ void rq_pass(chunk* __restrict__ f, chunk* __restrict__ b,
+                                        const fop* __restrict__ ops, const cx* __restrict__ mats,
+                                        fgeo fg, uint32_t l0, cx* __restrict__ partials,
+                                        uint64_t slot_stride) {
   constexpr int LOGNT = NT == 64 ? 6 : NT == 128 ? 7 : NT == 256 ? 8 : 9;
   constexpr int CPT = RQ_R / VEC;  // chunks of each state per thread (8)
   constexpr int TA = NT * RQ_R;    // amplitudes per tile and state
@@ -520,6 +531,11 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     }
   };
   auto run = [&](cx (&xf)[RQ_R], cx (&xb)[RQ_R]) __attribute__((always_inline)) {
+    if constexpr (!std::is_same<PROG, void>::value) {
+      static_assert(!TWO, "specialized passes of k_rq: one-state");
+      PROG{}(xf, SpecEnv{mats, ops, nullptr, t, reinterpret_cast<char*>(buf)});
+      return;
+    }
     // loop state kept small (register pressure): the current layout as a uniform offset into
     // the program; the per-thread LDS parts are recomputed at each relayout
     uint32_t lcur = l0;
@@ -670,6 +686,13 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     }
   }
 }
+template <bool TWO, int NT, bool PF>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF ? QDC_RQ_PF_WAVES : 4)))
+void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
+          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
+          uint64_t slot_stride) {
+  rq_pass<TWO, NT, PF>(f, b, ops, mats, fg, l0, partials, slot_stride);
+}
 
 // One wave per tile (k_rw): the same programs, layouts and HBM addressing as k_rq with NT
 // threads, run by one 64-lane wave.  Lane l holds the registers of k_rq's threads l + 64 e
@@ -699,13 +722,13 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 // per thread: four slots, and a third of the forward's VALU time went to relayouts with their
 // four-wave barriers), and the next tile's 16 chunks per lane prefetched into pinned VGPRs as in
 // k_rq (rq_ld / rq_vmwait_two), with a dynamic tail taken block-wide.
-template <bool TWO, int NE, bool PF, int W, bool S5 = false>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(
-    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES,
-    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES)))
-void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
-          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
-          uint64_t slot_stride) {
+// PROG (not void; non-prefetching instances): the pass program as straight-line stage calls
+// (qdc_spec.hpp) in place of the interpreted op loop.
+template <bool TWO, int NE, bool PF, int W, bool S5 = false, class PROG = void>
+__device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict__ b,
+                                        const fop* __restrict__ ops, const cx* __restrict__ mats,
+                                        fgeo fg, uint32_t l0, cx* __restrict__ partials,
+                                        uint64_t slot_stride) {
   static_assert(NE == 1 || NE == 2 || NE == 4, "k_rw: 1, 2 or 4 register groups");
   static_assert(!S5 || (NE == 2 && VEC == 2 && ((W == 1 && !PF) || (W == 2 && PF && !TWO))),
                 "five slots: f32 one-wave tiles, or the two-wave prefetching one-state tiles");
@@ -849,6 +872,15 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
     __builtin_amdgcn_wave_barrier();
   };
   auto run = [&](cx (&xf)[R], cx (&xb)[R]) __attribute__((always_inline)) {
+    if constexpr (!std::is_same<PROG, void>::value) {
+      static_assert(!PF, "specialized k_rw passes: non-prefetching instances");
+      const SpecEnv E{mats, ops, accw, lane, bufb};
+      if constexpr (TWO)
+        PROG{}(xf, xb, E);
+      else
+        PROG{}(xf, E);
+      return;
+    }
     uint32_t lcur = l0;
     uint32_t ri = 0;
     for (uint32_t j = 0; j < fg.nops; ++j) {
@@ -1066,6 +1098,15 @@ void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
       }
     }
   }
+}
+template <bool TWO, int NE, bool PF, int W, bool S5 = false>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(
+    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES,
+    (PF && TWO) ? 1 : (!TWO && !PF) ? QDC_RW_WAVES_ONE : QDC_RW_WAVES)))
+void k_rw(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ ops,
+          const cx* __restrict__ mats, fgeo fg, uint32_t l0, cx* __restrict__ partials,
+          uint64_t slot_stride) {
+  rw_pass<TWO, NE, PF, W, S5>(f, b, ops, mats, fg, l0, partials, slot_stride);
 }
 
 }  // namespace qdc

@@ -388,11 +388,12 @@ def rq_plan(tile_bits, stages, deps=None, precision=None, slots=4):
     return rows[0][3:3 + slots], steps, rows[-1][3:3 + slots]
 
 
-def spec_selftest(tile_bits, stages, deps=None):
-    """Compile the specialized reverse-pass kernel of a five-slot two-state f32 pass (host only:
-    the runtime's generator and hipcc, qdc_spec_selftest).  stages as for rq_plan.  Returns
+def spec_selftest(tile_bits, stages, deps=None, precision="f32"):
+    """Compile the specialized kernel of a pass (host only: the runtime's generator and hipcc,
+    qdc_spec_selftest): f32 tile_bits 11, a five-slot two-state reverse pass; 12, a four-slot
+    one-state forward pass; f64 10 two-state, 11 one-state.  stages as for rq_plan.  Returns
     (kernel name, code object path); raises RuntimeError with the runtime's message."""
-    lib = load("f32")
+    lib = load(precision)
     n = len(stages)
     kinds = (C.c_uint * n)(*[int(s[0]) for s in stages])
     t1 = (C.c_uint * n)(*[int(s[1]) for s in stages])

@@ -209,8 +209,9 @@ size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds, co
                    const unsigned* t2, const unsigned long long* deps, size_t n,
                    unsigned* steps, size_t cap);
 
-/* Test hook (host only): the specialized reverse-pass kernel of a five-slot two-state pass over
- * n stages (kinds / t1 / t2 / deps as qdc_rq_plan, every stage accumulating Gamma): the
+/* Test hook (host only): the specialized kernel of a pass over n stages (kinds / t1 / t2 / deps
+ * as qdc_rq_plan) — f32 tile_bits 11: a five-slot two-state reverse pass, every stage
+ * accumulating Gamma; 12: a four-slot one-state forward pass; f64: 10 two-state, 11 one-state: the
  * runtime's source generator and hipcc for gfx950, as a circuit call on a GPU box runs them
  * (qdc_jit.hpp), without loading the code object.  name_out (cap >= 128) receives the kernel
  * name, a NUL, then the code object's path.  Returns NULL, or an error message. */

@@ -63,3 +63,55 @@ def test_spec_kernel_resources_and_no_stage_copies(tmp_path):
     # the interpreted kernel copies ~63 register pairs after every stage; straight-line code
     # keeps at most a handful of moves in total
     assert body.count("v_mov_b64") < 32, body.count("v_mov_b64")
+
+
+def test_spec_forward_pass_kernel(tmp_path):
+    """One-state forward passes (k_rq<false, 256, true> with the program inlined): a
+    qdc_specf_ kernel, no scratch, within the generic kernel's 128 VGPRs."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(11)
+    stages, deps = random_pass(rng, 12, 12, brick=False)
+    name, obj = q.spec_selftest(12, stages, deps)
+    assert name.startswith("qdc_specf_") and os.path.getsize(obj) > 10000
+    src = os.path.join(os.path.dirname(obj), name + "." + str(os.getpid()) + ".hip")
+    csrc = os.path.join(os.path.dirname(q.__file__), "..", "csrc")
+    inc = os.path.join(csrc, "..", "..", "include")
+    asm = tmp_path / "k.s"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "-I" + inc, "-I" + csrc, "-S", "--cuda-device-only", "-o", str(asm), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = asm.read_text()
+    meta = text[text.index(".amdhsa_kernel " + name):]
+    assert int(meta.split(".amdhsa_next_free_vgpr")[1].split()[0]) <= 128
+    assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
+    # a tile no specialized kernel runs: refused
+    with pytest.raises(RuntimeError):
+        q.spec_selftest(13, stages, deps)
+
+
+@pytest.mark.parametrize("tile_bits,prefix", [(10, "qdc_spec_d_"), (11, "qdc_specf_d_")])
+def test_spec_f64_pass_kernels(tmp_path, tile_bits, prefix):
+    """f64 passes: two-state reverse (k_rw<true, 1, false, 1>, 2^10 tiles) and one-state
+    (k_rw<false, 1, false, 2>, 2^11 tiles) written out per program, compiled with -DQDC_F64:
+    no scratch, no per-stage copies, within 256 VGPRs."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(tile_bits)
+    stages, deps = random_pass(rng, tile_bits, 10, brick=False)
+    name, obj = q.spec_selftest(tile_bits, stages, deps, precision="f64")
+    assert name.startswith(prefix) and os.path.getsize(obj) > 10000
+    src = os.path.join(os.path.dirname(obj), name + "." + str(os.getpid()) + ".hip")
+    csrc = os.path.join(os.path.dirname(q.__file__), "..", "csrc")
+    inc = os.path.join(csrc, "..", "..", "include")
+    asm = tmp_path / "k.s"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-DQDC_F64",
+                        "-I" + inc, "-I" + csrc, "-S", "--cuda-device-only", "-o", str(asm), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = asm.read_text()
+    meta = text[text.index(".amdhsa_kernel " + name):]
+    assert int(meta.split(".amdhsa_next_free_vgpr")[1].split()[0]) <= 256
+    assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
+    body = text[text.index(name + ":"):]
+    body = body[:body.index(".Lfunc_end")]
+    assert body.count("v_mov_b64") < 32

@@ -40,6 +40,8 @@ def bench_name(kernel):
                ("fused_apply" if wf else "fused_density")
     if kernel.startswith("qdc_spec_"):  # a specialized reverse pass (csrc/qdc_spec.hpp)
         return "fused_reverse"
+    if kernel.startswith("qdc_specf_"):  # a specialized one-state forward pass
+        return "fused_apply"
     m = re.search(r"k_r[qw]<(true|false), \d+[^>]*>", kernel)
     if m:  # register-resident gate passes (qdc_rq.hpp): k_rq<TWO, NT, PF>, k_rw<TWO, NE, PF>
         return "fused_reverse" if m.group(1) == "true" else "fused_apply"

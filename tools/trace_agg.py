@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Aggregate a rocprofv3 --stats kernel table by the bench's kernel names (tools/pmc_summary.py
-bench_name): the specialized reverse passes (qdc_spec_<hash>, one symbol per pass program) and
-the interpreted k_rw both count as fused_reverse.  usage: trace_agg.py <trace_kernel_stats.csv>"""
+bench_name): the specialized passes (qdc_spec_<hash> reverse, qdc_specf_<hash> forward: one
+symbol per pass program) count with their interpreted kernels as fused_reverse / fused_apply.  usage: trace_agg.py <trace_kernel_stats.csv>"""
 import csv
 import sys
 from collections import defaultdict
