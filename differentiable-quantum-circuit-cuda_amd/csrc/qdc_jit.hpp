@@ -40,11 +40,15 @@ inline uint64_t spec_hash(const std::string& s) {
   return h;
 }
 
-// relayouts with immediate LDS offsets (spec_xchg_imm; QDC_SPEC_IMM=0: the XOR form)
+// relayouts with immediate LDS offsets (spec_xchg_imm, QDC_SPEC_IMM=1) instead of the XOR form.
+// Off by default: the immediate form's reads are bank-conflicted wherever the new layout's low
+// lane bits were slots before (its index is a pure bit permutation), and measured slower than
+// one v_xor per access on conflict-free swizzled addresses (r3q, C2 n = 28: reverse 2.569 vs
+// 2.537 ms, forward 1.278 vs 1.221 ms per launch)
 inline bool spec_imm() {
   static const int on = [] {
     const char* e = getenv("QDC_SPEC_IMM");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return on != 0;
 }
