@@ -325,6 +325,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_SPEC_MIN_QUBITS")) spec_min_qubits = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_MAX")) spec_max = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_FWD")) spec_fwd = atoi(e);
+    // the node's hipcc processes shared among the ranks of a multi-process job
+    SpecJit::get().set_processes(std::max(1, world / std::max(1, nlocal)));
 
     if (const char* e = getenv("QDC_FUSE_LCMIN"))
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
@@ -627,7 +629,6 @@ struct Circuit {
     uint32_t tbits = 0;  // amplitude bits of the tile
     // specialized kernel of a five-slot reverse pass or a one-state forward pass (qdc_jit.hpp): name, source, function
     SpecEntry* spec = nullptr;  // specialized kernel of the pass (qdc_jit.hpp), or none
-    hipFunction_t spec_fn = nullptr;
   };
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
   static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
@@ -989,7 +990,6 @@ struct Circuit {
       std::vector<SpecStep> sst;
       RqLayout lcur = P.load;
       it.spec = nullptr;
-      it.spec_fn = nullptr;
       for (const RqStep& step : P.steps) {
         if (!step.relayout && pslot[step.stage] >= 0)
           it.grad_slots.push_back((uint32_t)pslot[step.stage]);
@@ -1074,45 +1074,60 @@ struct Circuit {
     QDC_TRY(spec_load(items));
     return nullptr;
   }
-  // specialized passes: single-device, unsharded circuits of >= spec_min_qubits local qubits
-  bool spec_on() const {
-    return spec_mode > 0 && g == 0 && sh.size() == 1 && (spec_mode >= 2 || nl >= spec_min_qubits);
-  }
+  // specialized passes: circuits of >= spec_min_qubits local qubits (every shard runs the same
+  // program; the kernels are loaded on each shard's device)
+  bool spec_on() const { return spec_mode > 0 && (spec_mode >= 2 || nl >= spec_min_qubits); }
   // compile / load the kernels of this program's specialized passes (none when there are more
   // distinct ones than spec_max: deep random circuits would compile for minutes)
   const char* spec_load(std::vector<Item>& items) {
     if (items.empty()) return nullptr;
-    const int dev = sh[0].c().device;
-    std::vector<SpecEntry*> todo;  // distinct kernels of this call not loaded on dev yet
     size_t distinct = 0;
     ++spec_epoch;
-    for (Item& it : items) {
-      if (!it.spec) continue;
-      if (it.spec->epoch != spec_epoch) {
+    for (Item& it : items)
+      if (it.spec && it.spec->epoch != spec_epoch) {
         it.spec->epoch = spec_epoch;
         ++distinct;
-        if (!it.spec->fn.count(dev)) todo.push_back(it.spec);
       }
+    if (distinct == 0) return nullptr;
+    if (distinct > spec_max) {  // every pass of this call interpreted
+      for (Item& it : items) it.spec = nullptr;
+      return nullptr;
     }
-    if (distinct == 0 || distinct > spec_max) return nullptr;
-    if (!todo.empty()) {
+    std::vector<int> devs;
+    for (auto& s : sh)
+      if (std::find(devs.begin(), devs.end(), s.c().device) == devs.end()) devs.push_back(s.c().device);
+    for (size_t di = 0; di < devs.size(); ++di) {
+      const int dev = devs[di];
+      std::vector<SpecEntry*> todo;  // distinct kernels not loaded on dev yet
+      ++spec_epoch;
+      for (Item& it : items)
+        if (it.spec && it.spec->epoch != spec_epoch) {
+          it.spec->epoch = spec_epoch;
+          if (!it.spec->fn.count(dev)) todo.push_back(it.spec);
+        }
+      if (todo.empty()) continue;
       std::vector<std::string> names, srcs;
       for (const SpecEntry* e : todo) {
         names.push_back(e->name);
         srcs.push_back(e->src);
       }
-      QDC_TRY(sh[0].c().use());
+      for (auto& s : sh)
+        if (s.c().device == dev) {
+          QDC_TRY(s.c().use());
+          break;
+        }
       std::vector<hipFunction_t> fns;
       SpecJit::get().ensure(dev, names, srcs, fns);
       for (size_t k = 0; k < todo.size(); ++k)
         if (fns[k]) todo[k]->fn[dev] = fns[k];
     }
-    for (Item& it : items) {
-      if (!it.spec) continue;
-      auto f = it.spec->fn.find(dev);
-      it.spec_fn = f == it.spec->fn.end() ? nullptr : f->second;
-    }
     return nullptr;
+  }
+  // the pass's specialized kernel on a device, or none (the interpreted kernel runs)
+  static hipFunction_t spec_fn_on(const Item& it, int dev) {
+    if (!it.spec) return nullptr;
+    auto f = it.spec->fn.find(dev);
+    return f == it.spec->fn.end() ? nullptr : f->second;
   }
   // Run one fused group on every shard.  grads != nullptr: two-state reverse program whose
   // gradient gates write partials for gradient buffer rows var_idx[...].
@@ -1344,7 +1359,7 @@ struct Circuit {
       ctx.next_flops = flops;
       if (it.rq) {
         QDC_TRY(launch_rq(ctx, name, bytes, fg, two, it.tbits, it.l0, f, b, fops, mats, parts, stride,
-                          it.s5, it.spec_fn));
+                          it.s5, spec_fn_on(it, ctx.device)));
       } else if (two) {
         if (it.writes_f)
           QDC_TRY((launch_fused<true, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));

@@ -256,12 +256,18 @@ class SpecJit {
     return nullptr;
   }
   std::string code_object(const std::string& name) const { return obj_path(name); }
+  // processes of this job on the node (ranks): the default compile parallelism is shared
+  void set_processes(int p) {
+    std::lock_guard<std::mutex> lk(mu);
+    procs = std::max(procs, p);
+  }
 
  private:
   std::mutex mu;
   std::map<std::pair<int, std::string>, hipFunction_t> loaded;
   std::string hipcc, csrc, inc, dir;
   int state = 0;  // 0 unknown, 1 on, -1 off
+  int procs = 1;
   static bool exists(const std::string& p) {
     struct stat st;
     return stat(p.c_str(), &st) == 0;
@@ -313,7 +319,7 @@ class SpecJit {
   }
   bool compile(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
                const std::vector<size_t>& todo) {
-    int jobs = (int)std::thread::hardware_concurrency();
+    int jobs = std::min((int)std::thread::hardware_concurrency(), 16) / procs;
     if (const char* e = getenv("QDC_JIT_JOBS")) jobs = atoi(e);
     jobs = std::max(1, std::min(jobs, 16));
     struct Job {

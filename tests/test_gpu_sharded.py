@@ -201,3 +201,41 @@ def test_entry_points_keep_the_callers_device():
         del c
         assert _current_device() == caller, f"destructor moved the caller ({devs})"
     _set_device(0)
+
+
+@pytest.mark.parametrize("prec,kw", [("f32", {"local_shards": 4}), ("f32", {"devices": [0, 0]}),
+                                     ("f64", {"local_shards": 4})])
+def test_specialized_passes_sharded(prec, kw):
+    """Sharded circuits run the passes specialized per program too (csrc/qdc_spec.hpp; every
+    shard the same program, the kernel loaded on each shard's device): forced on (QDC_SPEC=2)
+    they match the interpreted kernels — f32 bit-identical, f64 within 1e-14 (two FMA
+    contractions of a complex product, tests/test_gpu_fusion.py) — and the oracle's floors."""
+    import quantum_differentiable_circuit as q
+    n = 18
+    ins, var = O.layered_circuit(n, 3, seed=41)
+    fl = F.Floor(prec, n, ins, [], var, run=False)
+    out = {}
+    for mode in ("0", "2"):
+        old = os.environ.get("QDC_SPEC")
+        os.environ["QDC_SPEC"] = mode
+        try:
+            c = build(q, prec, n, ins, **kw)
+        finally:
+            if old is None:
+                del os.environ["QDC_SPEC"]
+            else:
+                os.environ["QDC_SPEC"] = old
+        d = c.forward([], fl.var)
+        g = c.backward(fl.cots, [], fl.var)
+        what = f"C2 n={n} {prec} {kw} spec={mode} "
+        fl.check("forward", d, what)
+        fl.check("grads", g, what)
+        out[mode] = (np.asarray(d).reshape(-1),
+                     np.concatenate([np.asarray(x).reshape(-1) for x in g]))
+    for k, name in enumerate(("densities", "grads")):
+        a0, a2 = out["0"][k], out["2"][k]
+        if prec == "f32":
+            assert np.array_equal(a0, a2), f"{kw}: specialized {name} differ"
+        else:
+            rel = np.linalg.norm(a2 - a0) / max(np.linalg.norm(a0), 1e-300)
+            assert rel <= 1e-14, f"{kw}: specialized {name} differ by {rel:.2e}"
