@@ -161,17 +161,37 @@ def test_devices_rccl_single_process():
     fl.check("grads", c.backward(fl.cots, [], fl.var), "devices=2 ")
 
 
+def _hip():
+    """The HIP runtime the circuit library itself is linked against (libqdc's RUNPATH, already
+    mapped): a bare dlopen("libamdhip64.so") can bind torch's bundled copy of the runtime, a
+    second instance with its own device state."""
+    import ctypes
+    from quantum_differentiable_circuit import _native
+    _native.load("f32")
+    for line in open("/proc/self/maps"):
+        path = line.split()[-1]
+        if "libamdhip64" in path and "/torch/" not in path:
+            return ctypes.CDLL(path)
+    raise RuntimeError("the circuit library's HIP runtime is not mapped")
+
+
 def _current_device():
     import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
     d = ctypes.c_int(-1)
-    assert hip.hipGetDevice(ctypes.byref(d)) == 0
+    assert _hip().hipGetDevice(ctypes.byref(d)) == 0
     return d.value
 
 
 def _set_device(i):
     import ctypes
-    assert ctypes.CDLL("libamdhip64.so").hipSetDevice(ctypes.c_int(i)) == 0
+    assert _hip().hipSetDevice(ctypes.c_int(i)) == 0
+
+
+def _device_count():
+    import ctypes
+    n = ctypes.c_int(0)
+    assert _hip().hipGetDeviceCount(ctypes.byref(n)) == 0
+    return n.value
 
 
 def test_entry_points_keep_the_callers_device():
@@ -180,14 +200,13 @@ def test_entry_points_keep_the_callers_device():
     caller's code must not find themselves on the last shard's GPU afterwards.  On one GPU the
     repeated-device circuit covers the per-shard contexts; with two GPUs the circuit lives on
     device 1 while the caller stays on device 0 (and the reverse)."""
-    import torch
     import quantum_differentiable_circuit as q
     n = 10
     ins, var = O.layered_circuit(n, layers=1, seed=3)
     vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
     cots = F.sigma_z_cots([np.zeros((2, 2))] * n, np.complex64)
     cases = [([0, 0], 0)]
-    if torch.cuda.device_count() >= 2:
+    if _device_count() >= 2:
         cases += [([1], 0), ([0], 1), ([0, 1], 1)]
     for devs, caller in cases:
         _set_device(caller)
