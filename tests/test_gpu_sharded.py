@@ -162,17 +162,22 @@ def test_devices_rccl_single_process():
 
 
 def _hip():
-    """The HIP runtime the circuit library itself is linked against (libqdc's RUNPATH, already
-    mapped): a bare dlopen("libamdhip64.so") can bind torch's bundled copy of the runtime, a
+    """The HIP runtime instance the circuit library is bound to.  torch bundles its own copy with
+    the same soname: loaded first, it is the one libqdc binds (ROCm's is then never mapped), else
+    libqdc maps ROCm's through its RUNPATH.  A bare dlopen("libamdhip64.so") may instead open a
     second instance with its own device state."""
     import ctypes
     from quantum_differentiable_circuit import _native
     _native.load("f32")
+    mapped = []
     for line in open("/proc/self/maps"):
         path = line.split()[-1]
-        if "libamdhip64" in path and "/torch/" not in path:
-            return ctypes.CDLL(path)
-    raise RuntimeError("the circuit library's HIP runtime is not mapped")
+        if "libamdhip64" in path and path not in mapped:
+            mapped.append(path)
+    if not mapped:
+        raise RuntimeError("no HIP runtime is mapped")
+    own = [p for p in mapped if "/torch/" not in p]
+    return ctypes.CDLL((own or mapped)[0])
 
 
 def _current_device():
