@@ -1074,15 +1074,9 @@ struct Circuit {
     QDC_TRY(spec_load(items));
     return nullptr;
   }
-  // specialized passes: unsharded circuits of >= spec_min_qubits qubits, or any circuit when
-  // forced (every shard runs the same program; the kernels are loaded on each shard's device)
-  // Sharded circuits (g > 0 or several shards) only when forced (QDC_SPEC=2): every rank of a
-  // multi-process job would compile the same kernels at its first call, and the path has run
-  // on one GPU's local shards only.
-  bool spec_on() const {
-    if (spec_mode >= 2) return true;
-    return spec_mode == 1 && g == 0 && sh.size() == 1 && nl >= spec_min_qubits;
-  }
+  // specialized passes: circuits of >= spec_min_qubits local qubits (every shard runs the same
+  // program; the kernels are loaded on each shard's device)
+  bool spec_on() const { return spec_mode > 0 && (spec_mode >= 2 || nl >= spec_min_qubits); }
   // compile / load the kernels of this program's specialized passes (none when there are more
   // distinct ones than spec_max: deep random circuits would compile for minutes)
   const char* spec_load(std::vector<Item>& items) {
