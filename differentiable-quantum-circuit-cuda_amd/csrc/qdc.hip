@@ -530,6 +530,38 @@ QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds,
   return nullptr;
 }
 
+QDC_API size_t qdc_jit_stats(double* stats, size_t n) {
+  const qdc::JitStats s = qdc::SpecJit::get().counters();
+  const bool on = qdc::SpecJit::get().enabled();
+  const double v[8] = {(double)s.compiled, (double)s.waited, (double)s.loaded, s.compile_s,
+                       s.wait_s, s.ensure_s, on ? 1.0 : 0.0,
+                       (double)qdc::Ctx::spec_launches().load(std::memory_order_relaxed)};
+  size_t k = 0;
+  for (; stats && k < n && k < 8; ++k) stats[k] = v[k];
+  return k;
+}
+
+QDC_API const char* qdc_jit_dir(char* dir_out, size_t cap) {
+  if (!dir_out || cap < 2) return "invalid arguments";
+  const std::string d = qdc::SpecJit::get().cache_dir();
+  if (d.empty()) return "specialized passes are off (see the message on stderr)";
+  if (d.size() + 1 > cap) return "buffer too small";
+  std::memcpy(dir_out, d.c_str(), d.size() + 1);
+  return nullptr;
+}
+
+QDC_API const char* qdc_spec_fingerprint(const char* defines, const char* compiler,
+                                         const char* csrc_dir, unsigned long long* fingerprint,
+                                         unsigned long long* source_hash) {
+  if (!compiler || !csrc_dir || !fingerprint) return "invalid arguments";
+  uint64_t sfp = 0;
+  const std::string cs = csrc_dir;
+  if (!qdc::spec_source_fp(cs, cs + "/../../include", sfp)) return "cannot read the kernel headers";
+  *fingerprint = qdc::spec_fingerprint(defines ? std::string(defines) : qdc::spec_defines(), compiler, sfp);
+  if (source_hash) *source_hash = sfp;
+  return nullptr;
+}
+
 QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds,
                            const unsigned* t1, const unsigned* t2,
                            const unsigned long long* deps, size_t n, unsigned* steps,

@@ -6,6 +6,8 @@
 // context per stream that owns every scratch buffer for its lifetime.
 #pragma once
 
+#include <atomic>
+
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -301,6 +303,12 @@ struct Ctx {
     return nullptr;
   }
 
+  // launches of specialized kernels in this process (qdc_jit_stats: tests check that a forced
+  // specialized run launched them, not the interpreted kernels)
+  static std::atomic<uint64_t>& spec_launches() {
+    static std::atomic<uint64_t> n{0};
+    return n;
+  }
   // a kernel from a loaded code object (qdc_jit.hpp), arguments as for launch_block
   template <typename... Args>
   const char* launch_module(const char* name, double bytes, hipFunction_t fn, uint32_t grid,
@@ -317,6 +325,7 @@ struct Ctx {
     if (e != hipSuccess)
       return fail("HIP ERROR: launch of kernel %s (specialized) failed with %s.", name,
                   hipGetErrorName(e));
+    spec_launches().fetch_add(1, std::memory_order_relaxed);
     if (prof.on && a && b) {
       (void)hipEventRecord(b, stream);
       prof.recs.push_back({name, bytes, next_flops, a, b});

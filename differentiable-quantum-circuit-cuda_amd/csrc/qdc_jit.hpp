@@ -2,23 +2,33 @@
 // one-state forward passes): source per pass program, compiled with hipcc for gfx950 on first
 // use, cached on disk and per device.
 //
-// A pass program becomes a functor of straight-line stage calls; its source text (hashed)
-// names the kernel, so passes with the same program share one kernel, across circuits and
-// processes (the code objects live in QDC_JIT_DIR, default /tmp/qdc_jit_<uid>).  The missing
-// kernels of a call are compiled in parallel child processes (posix_spawn of hipcc; the
-// calling process never execs), then loaded with hipModuleLoad.  Any failure (no hipcc, a
-// compile error, a load error) turns specialization off for the process with one message on
-// stderr: the generic kernel then runs every pass, as it does for passes the cap leaves out.
+// A pass program becomes a functor of straight-line stage calls.  Its kernel is named by the
+// hash of its source and of the build fingerprint (the library's -D switches, hipcc's path and
+// --version text, the compile options, and the bytes of every kernel header), so passes with
+// the same program share one kernel across circuits and processes, and no two builds ever share
+// one.  Code objects live in a private cache directory (QDC_JIT_DIR, else $XDG_CACHE_HOME/qdc_jit,
+// $HOME/.cache/qdc_jit or /tmp/qdc_jit_<uid>: owned by this user, not writable by others), each
+// behind a header that names its fingerprint and kernel and hashes its bytes; ensure() loads
+// only objects whose header matches.  The missing kernels of a call are compiled in parallel
+// child processes (posix_spawn of hipcc; the calling process never execs); one process of a job
+// compiles each kernel (a per-kernel flock), the others wait and load it.  Any failure (no
+// hipcc, headers changed since the library was built, a compile or load error) turns
+// specialization off for the process with one message on stderr: the generic kernel then runs
+// every pass, as it does for passes the cap leaves out.
 #pragma once
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <spawn.h>
+#include <sys/file.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <ctime>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -160,13 +170,6 @@ inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint3
   }
   return b;
 }
-// kernel name (prefix + hash of the generic kernel and the program) and source
-inline std::string spec_kernel_name(const std::string& body, const SpecKind& K) {
-  char nm[48];
-  snprintf(nm, sizeof nm, "%s%016llx", K.prefix,
-           (unsigned long long)spec_hash(std::string(K.pass) + "\n" + body));
-  return nm;
-}
 inline std::string spec_kernel_source(const std::string& name, const std::string& body, const SpecKind& K) {
   const std::string R = std::to_string(1u << K.ns);
   const std::string args =
@@ -197,17 +200,126 @@ struct SpecEntry {
   uint64_t epoch = 0;  // last call (spec_load) that counted it
 };
 
+// FNV-1a continued over more bytes
+inline uint64_t fnv_more(uint64_t h, const void* p, size_t n) {
+  const unsigned char* c = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  return h;
+}
+inline bool read_file(const std::string& path, std::string& out) {
+  FILE* fp = fopen(path.c_str(), "rb");
+  if (!fp) return false;
+  out.clear();
+  char b[65536];
+  size_t k;
+  while ((k = fread(b, 1, sizeof b, fp)) > 0) out.append(b, k);
+  const bool ok = !ferror(fp);
+  fclose(fp);
+  return ok;
+}
+
+// The kernel headers a generated source compiles against: every csrc/*.hpp and include/qdc/*.h,
+// hashed as (relative path, NUL, bytes, NUL) in sorted path order.  csrc/src_fp.py computes the
+// same at build time (QDC_SRC_FP), so a library can tell that the headers next to it are no
+// longer the ones it was built from.
+inline bool spec_source_fp(const std::string& csrc, const std::string& inc, uint64_t& out) {
+  std::vector<std::pair<std::string, std::string>> files;  // (relative name, path)
+  auto scan = [&](const std::string& dir, const std::string& rel, const char* ext) {
+    DIR* d = opendir(dir.c_str());
+    if (!d) return false;
+    const size_t el = strlen(ext);
+    while (dirent* e = readdir(d)) {
+      const std::string nm = e->d_name;
+      if (nm.size() > el && nm.compare(nm.size() - el, el, ext) == 0 && nm[0] != '.')
+        files.emplace_back(rel + nm, dir + "/" + nm);
+    }
+    closedir(d);
+    return true;
+  };
+  if (!scan(csrc, "csrc/", ".hpp") || !scan(inc + "/qdc", "include/qdc/", ".h")) return false;
+  std::sort(files.begin(), files.end());
+  uint64_t h = 1469598103934665603ull;
+  std::string body;
+  for (const auto& f : files) {
+    if (!read_file(f.second, body)) return false;
+    h = fnv_more(h, f.first.c_str(), f.first.size() + 1);
+    h = fnv_more(h, body.data(), body.size());
+    h = fnv_more(h, "", 1);
+  }
+  out = h;
+  return true;
+}
+
+// the library's own compile-time switches, so the kernels agree with it
+inline std::string spec_defines() {
+  char b[512];
+  snprintf(b, sizeof b,
+           "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
+           "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d%s",
+           (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
+           (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
+           sizeof(real) == 8 ? " -DQDC_F64" : "");
+  return b;
+}
+// hipcc options of every specialized kernel besides the defines and include paths
+inline const char* spec_cflags() { return "--genco -O3 -std=c++17 --offload-arch=gfx950"; }
+// The build fingerprint that goes into every kernel name: the defines, the compiler's identity
+// (its path and --version text), the options and the header bytes.  Two libraries that differ
+// in any of them never share a code object in one cache directory.
+inline uint64_t spec_fingerprint(const std::string& defines, const std::string& compiler,
+                                 uint64_t source_fp) {
+  uint64_t h = 1469598103934665603ull;
+  const std::string s = defines + "\n" + compiler + "\n" + spec_cflags() + "\n";
+  h = fnv_more(h, s.data(), s.size());
+  return fnv_more(h, &source_fp, sizeof source_fp);
+}
+// kernel name: prefix + hash of the build fingerprint, the generic kernel and the program
+inline std::string spec_kernel_name_fp(const std::string& body, const SpecKind& K, uint64_t fp) {
+  char nm[48];
+  uint64_t h = spec_hash(std::string(K.pass) + "\n" + body);
+  h = fnv_more(h, &fp, sizeof fp);
+  snprintf(nm, sizeof nm, "%s%016llx", K.prefix, (unsigned long long)h);
+  return nm;
+}
+
+#ifndef QDC_SRC_FP
+#define QDC_SRC_FP 0ull  // not built by csrc/Makefile: the header check is skipped
+#endif
+
+// A code object on disk: this header, then hipcc's output.  ensure() loads an object only when
+// the header names the current build fingerprint and the kernel, and the bytes are whole.
+struct JitObjHeader {
+  char magic[8];
+  uint64_t fp, name_hash, size, body_hash;
+};
+static_assert(sizeof(JitObjHeader) == 40, "code-object header layout");
+constexpr char JIT_MAGIC[8] = {'Q', 'D', 'C', 'J', 'I', 'T', '2', '\0'};
+
+// counters of this process's specialized-kernel cache (qdc_jit_stats)
+struct JitStats {
+  uint64_t compiled = 0;  // kernels this process compiled
+  uint64_t waited = 0;    // kernels another process was compiling when this one needed them
+  uint64_t loaded = 0;    // (kernel, device) loads
+  double compile_s = 0, wait_s = 0, ensure_s = 0;
+};
+
 class SpecJit {
  public:
   static SpecJit& get() {
     static SpecJit j;
     return j;
   }
+  // the build fingerprint (0 while specialization is off)
+  uint64_t fingerprint() {
+    std::lock_guard<std::mutex> lk(mu);
+    return init() ? fp : 0;
+  }
   // Kernels of the given names / sources on `device` (the current device), compiling and
   // loading the missing ones; fns[i] = nullptr where specialization is off.
   void ensure(int device, const std::vector<std::string>& names,
               const std::vector<std::string>& srcs, std::vector<hipFunction_t>& fns) {
     std::lock_guard<std::mutex> lk(mu);
+    const double t0 = now();
     fns.assign(names.size(), nullptr);
     if (!init()) return;
     std::vector<size_t> todo;
@@ -219,43 +331,58 @@ class SpecJit {
       }
       bool dup = false;
       for (size_t k : todo) dup = dup || names[k] == names[i];
-      if (!dup && !exists(obj_path(names[i]))) todo.push_back(i);
+      if (!dup && !image(names[i])) todo.push_back(i);
     }
-    if (!todo.empty() && !compile(names, srcs, todo)) return;
+    if (!todo.empty() && !obtain(names, srcs, todo)) {
+      stats.ensure_s += now() - t0;
+      return;
+    }
     for (size_t i = 0; i < names.size(); ++i) {
       if (fns[i]) continue;
       auto it = loaded.find({device, names[i]});
       if (it == loaded.end()) {
         hipModule_t mod = nullptr;
         hipFunction_t fn = nullptr;
-        if (hipModuleLoad(&mod, obj_path(names[i]).c_str()) != hipSuccess ||
+        const std::vector<char>* img = image(names[i]);
+        if (!img || hipModuleLoadData(&mod, img->data()) != hipSuccess ||
             hipModuleGetFunction(&fn, mod, names[i].c_str()) != hipSuccess) {
           (void)hipGetLastError();
           disable("cannot load " + obj_path(names[i]));
           fns.assign(names.size(), nullptr);
+          stats.ensure_s += now() - t0;
           return;
         }
+        ++stats.loaded;
         it = loaded.emplace(std::make_pair(device, names[i]), fn).first;
       }
       fns[i] = it->second;
     }
+    stats.ensure_s += now() - t0;
   }
   bool enabled() {
     std::lock_guard<std::mutex> lk(mu);
     return init();
   }
-  // compile without loading (host-only test hook): true when every code object exists after
+  // compile without loading (host-only test hook): nullptr when every code object is valid after
   const char* compile_only(const std::vector<std::string>& names,
                            const std::vector<std::string>& srcs) {
     std::lock_guard<std::mutex> lk(mu);
-    if (!init()) return "specialization unavailable (no hipcc or kernel sources)";
+    if (!init()) return "specialization unavailable (no hipcc, kernel sources or cache directory)";
     std::vector<size_t> todo;
     for (size_t i = 0; i < names.size(); ++i)
-      if (!exists(obj_path(names[i]))) todo.push_back(i);
-    if (!todo.empty() && !compile(names, srcs, todo)) return "hipcc failed";
+      if (!image(names[i])) todo.push_back(i);
+    if (!todo.empty() && !obtain(names, srcs, todo)) return "hipcc failed";
     return nullptr;
   }
   std::string code_object(const std::string& name) const { return obj_path(name); }
+  std::string cache_dir() {
+    std::lock_guard<std::mutex> lk(mu);
+    return init() ? dir : std::string();
+  }
+  JitStats counters() {
+    std::lock_guard<std::mutex> lk(mu);
+    return stats;
+  }
   // processes of this job on the node (ranks): the default compile parallelism is shared
   void set_processes(int p) {
     std::lock_guard<std::mutex> lk(mu);
@@ -265,17 +392,120 @@ class SpecJit {
  private:
   std::mutex mu;
   std::map<std::pair<int, std::string>, hipFunction_t> loaded;
+  std::map<std::string, std::vector<char>> images;  // validated code objects (kept for the process)
   std::string hipcc, csrc, inc, dir;
+  uint64_t fp = 0;
   int state = 0;  // 0 unknown, 1 on, -1 off
   int procs = 1;
-  static bool exists(const std::string& p) {
-    struct stat st;
-    return stat(p.c_str(), &st) == 0;
+  JitStats stats;
+  static double now() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
   }
-  std::string obj_path(const std::string& name) const { return dir + "/" + name + ".hsaco"; }
+  std::string obj_path(const std::string& name) const { return dir + "/" + name + ".qco"; }
+  std::string lock_path(const std::string& name) const { return dir + "/" + name + ".lock"; }
   void disable(const std::string& why) {
     if (state != -1) fprintf(stderr, "qdc: specialized passes off (%s)\n", why.c_str());
     state = -1;
+  }
+  // the validated code object of `name` (cached in memory), or nullptr when the file is
+  // missing, from another build, truncated or otherwise not this kernel's
+  const std::vector<char>* image(const std::string& name) {
+    auto it = images.find(name);
+    if (it != images.end()) return &it->second;
+    std::string raw;
+    if (!read_file(obj_path(name), raw) || raw.size() <= sizeof(JitObjHeader)) return nullptr;
+    JitObjHeader h;
+    memcpy(&h, raw.data(), sizeof h);
+    const char* body = raw.data() + sizeof h;
+    const size_t n = raw.size() - sizeof h;
+    if (memcmp(h.magic, JIT_MAGIC, 8) != 0 || h.fp != fp || h.name_hash != spec_hash(name) ||
+        h.size != n || h.body_hash != fnv_more(1469598103934665603ull, body, n))
+      return nullptr;
+    return &images.emplace(name, std::vector<char>(body, body + n)).first->second;
+  }
+  // A cache directory no other user can write into: not a symlink, owned by this user, not
+  // group/world-writable (a default location: no group/world access at all).
+  static bool secure_dir(const std::string& d, bool strict, std::string& why) {
+    mkdir(d.c_str(), 0700);
+    struct stat st;
+    if (lstat(d.c_str(), &st) != 0) {
+      why = d + ": cannot be created";
+      return false;
+    }
+    if (S_ISLNK(st.st_mode) || !S_ISDIR(st.st_mode)) {
+      why = d + ": not a directory";
+      return false;
+    }
+    if (st.st_uid != geteuid()) {
+      why = d + ": owned by another user";
+      return false;
+    }
+    if (st.st_mode & (strict ? 077 : 022)) {
+      why = d + (strict ? ": accessible to other users" : ": writable by other users");
+      return false;
+    }
+    if (access(d.c_str(), W_OK | X_OK) != 0) {
+      why = d + ": not writable";
+      return false;
+    }
+    return true;
+  }
+  // QDC_JIT_DIR, else $XDG_CACHE_HOME/qdc_jit, $HOME/.cache/qdc_jit, /tmp/qdc_jit_<uid>: the
+  // first that passes secure_dir
+  bool choose_dir(std::string& why) {
+    if (const char* d = getenv("QDC_JIT_DIR")) {
+      dir = d;
+      return secure_dir(dir, false, why);
+    }
+    std::vector<std::string> cand;
+    const char* xdg = getenv("XDG_CACHE_HOME");
+    if (xdg && xdg[0] == '/') cand.push_back(std::string(xdg) + "/qdc_jit");
+    const char* home = getenv("HOME");
+    if (home && home[0] == '/') {
+      mkdir((std::string(home) + "/.cache").c_str(), 0700);
+      cand.push_back(std::string(home) + "/.cache/qdc_jit");
+    }
+    cand.push_back("/tmp/qdc_jit_" + std::to_string((unsigned)geteuid()));
+    std::string w;
+    for (const std::string& c : cand) {
+      if (secure_dir(c, true, w)) {
+        dir = c;
+        return true;
+      }
+      why += (why.empty() ? "" : "; ") + w;
+    }
+    return false;
+  }
+  // the standard output + error of a child (posix_spawn: this process never execs)
+  static bool run_capture(const std::vector<std::string>& args, std::string& out) {
+    int fd[2];
+    if (pipe(fd) != 0) return false;
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_adddup2(&fa, fd[1], 1);
+    posix_spawn_file_actions_adddup2(&fa, fd[1], 2);
+    posix_spawn_file_actions_addclose(&fa, fd[0]);
+    posix_spawn_file_actions_addclose(&fa, fd[1]);
+    std::vector<char*> argv;
+    for (const std::string& a : args) argv.push_back(const_cast<char*>(a.c_str()));
+    argv.push_back(nullptr);
+    pid_t pid = 0;
+    const int rc = posix_spawn(&pid, args[0].c_str(), &fa, nullptr, argv.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    close(fd[1]);
+    out.clear();
+    if (rc == 0) {
+      char b[4096];
+      ssize_t k;
+      while ((k = read(fd[0], b, sizeof b)) > 0 || (k < 0 && errno == EINTR))
+        if (k > 0) out.append(b, (size_t)k);
+    }
+    close(fd[0]);
+    int status = 0;
+    if (rc != 0 || waitpid(pid, &status, 0) < 0) return false;
+    return WIFEXITED(status) && WEXITSTATUS(status) == 0;
   }
   bool init() {
     if (state) return state > 0;
@@ -296,82 +526,180 @@ class SpecJit {
     const char* h = getenv("QDC_HIPCC");
     const char* rp = getenv("ROCM_PATH");
     hipcc = h ? h : (rp ? std::string(rp) + "/bin/hipcc" : "/opt/rocm/bin/hipcc");
-    const char* d = getenv("QDC_JIT_DIR");
-    dir = d ? d : "/tmp/qdc_jit_" + std::to_string((unsigned)getuid());
-    mkdir(dir.c_str(), 0700);
-    if (!exists(csrc + "/qdc_spec.hpp") || access(hipcc.c_str(), X_OK) != 0 || !exists(dir)) {
+    if (!exists(csrc + "/qdc_spec.hpp") || access(hipcc.c_str(), X_OK) != 0) {
       disable("no hipcc or kernel sources next to the library");
       return false;
     }
+    uint64_t sfp = 0;
+    if (!spec_source_fp(csrc, inc, sfp)) {
+      disable("cannot read the kernel headers in " + csrc);
+      return false;
+    }
+    if ((uint64_t)QDC_SRC_FP != 0 && sfp != (uint64_t)QDC_SRC_FP) {
+      disable("the kernel headers in " + csrc + " are not the ones this library was built from");
+      return false;
+    }
+    std::string ver;
+    if (!run_capture({hipcc, "--version"}, ver)) {
+      disable(hipcc + " --version failed");
+      return false;
+    }
+    std::string why;
+    if (!choose_dir(why)) {
+      disable("no private cache directory (" + why + ")");
+      return false;
+    }
+    fp = spec_fingerprint(spec_defines(), hipcc + "\n" + ver, sfp);
     state = 1;
     return true;
   }
-  // the library's own compile-time switches, so the kernels agree with it
-  static std::string defines() {
-    char b[512];
-    snprintf(b, sizeof b,
-             "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
-             "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d%s",
-             (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
-             (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-             sizeof(real) == 8 ? " -DQDC_F64" : "");
-    return b;
+  static bool exists(const std::string& p) {
+    struct stat st;
+    return stat(p.c_str(), &st) == 0;
+  }
+  // The missing kernels `todo`: one process compiles each.  A kernel whose lock this process
+  // takes (flock, released by the kernel if the holder dies) and whose object is still missing
+  // is compiled here, in parallel with the others taken; a kernel another process holds is
+  // waited for, then loaded — or compiled here if that process failed.
+  bool obtain(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
+              const std::vector<size_t>& todo) {
+    std::vector<size_t> mine;
+    std::vector<int> held;
+    std::vector<std::pair<size_t, int>> others;
+    auto release = [](int fd) {
+      flock(fd, LOCK_UN);
+      close(fd);
+    };
+    for (size_t i : todo) {
+      const int fd = open(lock_path(names[i]).c_str(), O_RDWR | O_CREAT | O_CLOEXEC | O_NOFOLLOW, 0600);
+      if (fd < 0) {
+        for (int h : held) release(h);
+        for (auto& o : others) close(o.second);
+        disable("cannot create " + lock_path(names[i]));
+        return false;
+      }
+      if (flock(fd, LOCK_EX | LOCK_NB) == 0) {
+        if (image(names[i])) {  // finished by another process meanwhile
+          release(fd);
+          continue;
+        }
+        mine.push_back(i);
+        held.push_back(fd);
+      } else {
+        others.emplace_back(i, fd);
+      }
+    }
+    bool ok = mine.empty() || compile(names, srcs, mine);
+    for (int h : held) release(h);
+    double wait_lim = 900;
+    if (const char* e = getenv("QDC_JIT_WAIT_S")) wait_lim = atof(e);
+    for (auto& o : others) {
+      if (!ok) {
+        close(o.second);
+        continue;
+      }
+      const double t0 = now();
+      ++stats.waited;
+      while (flock(o.second, LOCK_EX | LOCK_NB) != 0) {
+        if (now() - t0 > wait_lim) {
+          close(o.second);
+          disable("timed out waiting for another process compiling " + names[o.first]);
+          ok = false;
+          break;
+        }
+        usleep(20000);
+      }
+      stats.wait_s += now() - t0;
+      if (!ok) continue;
+      if (!image(names[o.first])) ok = compile(names, srcs, {o.first});
+      release(o.second);
+    }
+    return ok;
+  }
+  // write `elf` as the code object of `name` (header + bytes) by atomic rename
+  bool publish(const std::string& name, const std::string& elf, const std::string& tag) {
+    JitObjHeader h;
+    memcpy(h.magic, JIT_MAGIC, 8);
+    h.fp = fp;
+    h.name_hash = spec_hash(name);
+    h.size = elf.size();
+    h.body_hash = fnv_more(1469598103934665603ull, elf.data(), elf.size());
+    const std::string tmp = obj_path(name) + "." + tag + ".tmp";
+    FILE* fo = fopen(tmp.c_str(), "wb");
+    if (!fo) return false;
+    bool ok = fwrite(&h, sizeof h, 1, fo) == 1 && fwrite(elf.data(), 1, elf.size(), fo) == elf.size();
+    ok = (fclose(fo) == 0) && ok;
+    if (!ok || rename(tmp.c_str(), obj_path(name).c_str()) != 0) {
+      unlink(tmp.c_str());
+      return false;
+    }
+    return true;
   }
   bool compile(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
                const std::vector<size_t>& todo) {
+    const double t0 = now();
     int jobs = std::min((int)std::thread::hardware_concurrency(), 16) / procs;
     if (const char* e = getenv("QDC_JIT_JOBS")) jobs = atoi(e);
     jobs = std::max(1, std::min(jobs, 16));
+    const char* keep_env = getenv("QDC_JIT_KEEP");  // keep sources and logs of good compiles
+    const bool keep = keep_env && atoi(keep_env) != 0;
     struct Job {
       pid_t pid;
       size_t i;
-      std::string tmp;
+      std::string src, out;
     };
     std::vector<Job> run;
     size_t next = 0;
     bool ok = true;
     const std::string tag = std::to_string((long)getpid());
+    const std::string defs = spec_defines(), flags = spec_cflags();
     auto reap = [&]() {
       int status = 0;
       const pid_t p = waitpid(run.front().pid, &status, 0);
       Job j = run.front();
       run.erase(run.begin());
-      const std::string obj = obj_path(names[j.i]);
-      if (p < 0 || !WIFEXITED(status) || WEXITSTATUS(status) != 0 || rename(j.tmp.c_str(), obj.c_str()) != 0) {
-        ok = false;
-        unlink(j.tmp.c_str());
+      std::string elf;
+      const bool good = p >= 0 && WIFEXITED(status) && WEXITSTATUS(status) == 0 &&
+                        read_file(j.out, elf) && !elf.empty() && publish(names[j.i], elf, tag);
+      unlink(j.out.c_str());
+      if (!good) {
+        ok = false;  // the source and the log stay for inspection
+        return;
+      }
+      ++stats.compiled;
+      if (!keep) {
+        unlink(j.src.c_str());
+        unlink((j.src + ".log").c_str());
       }
     };
     while (next < todo.size() || !run.empty()) {
       if (ok && next < todo.size() && (int)run.size() < jobs) {
         const size_t i = todo[next++];
-        const std::string src = dir + "/" + names[i] + "." + tag + ".hip";
-        FILE* fp = fopen(src.c_str(), "w");
-        if (!fp) {
+        Job j{0, i, dir + "/" + names[i] + "." + tag + ".hip", dir + "/" + names[i] + "." + tag + ".elf"};
+        FILE* fp_src = fopen(j.src.c_str(), "w");
+        if (!fp_src) {
           ok = false;
           continue;
         }
-        fputs(srcs[i].c_str(), fp);
-        fclose(fp);
-        Job j{0, i, obj_path(names[i]) + "." + tag};
-        std::vector<std::string> args = {hipcc, "--genco", "-O3", "-std=c++17", "--offload-arch=gfx950",
-                                         "-I" + inc, "-I" + csrc, "-o", j.tmp, src};
-        {
-          std::string d = defines();
+        fputs(srcs[i].c_str(), fp_src);
+        fclose(fp_src);
+        std::vector<std::string> args = {hipcc};
+        for (const std::string* s : {&flags, &defs}) {
           size_t p = 0;
-          while (p < d.size()) {
-            size_t q = d.find(' ', p);
-            if (q == std::string::npos) q = d.size();
-            args.insert(args.begin() + 5, d.substr(p, q - p));
+          while (p < s->size()) {
+            size_t q = s->find(' ', p);
+            if (q == std::string::npos) q = s->size();
+            if (q > p) args.push_back(s->substr(p, q - p));
             p = q + 1;
           }
         }
+        for (const std::string& a : {"-I" + inc, "-I" + csrc, std::string("-o"), j.out, j.src}) args.push_back(a);
         std::vector<char*> argv;
         for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
         argv.push_back(nullptr);
         posix_spawn_file_actions_t fa;
         posix_spawn_file_actions_init(&fa);
-        const std::string log = src + ".log";
+        const std::string log = j.src + ".log";
         posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
         posix_spawn_file_actions_adddup2(&fa, 1, 2);
         const int rc = posix_spawn(&j.pid, hipcc.c_str(), &fa, nullptr, argv.data(), environ);
@@ -386,9 +714,15 @@ class SpecJit {
       if (!run.empty()) reap();
       else break;
     }
+    stats.compile_s += now() - t0;
     if (!ok) disable("hipcc failed on a pass kernel (sources and logs in " + dir + ")");
     return ok;
   }
 };
+
+// kernel name of a program under this library's build fingerprint
+inline std::string spec_kernel_name(const std::string& body, const SpecKind& K) {
+  return spec_kernel_name_fp(body, K, SpecJit::get().fingerprint());
+}
 
 }  // namespace qdc

@@ -20,12 +20,13 @@ from typing import List, Sequence
 
 import numpy as np
 
+from .common_gates import get_cnot, get_hadamard  # noqa: E402  (common_gates.rs)
 from ._native import (PanicException, KernelStat, PlanOp, check, default_precision, load,
                       ptr, PRECISIONS)
 
 __all__ = ["Circuit", "Circuit32", "Circuit64", "QuantizedTensor", "PanicException",
            "get_q1_grad", "get_q2_grad", "get_q2_grad_diag", "data_transfer", "circuit_class",
-           "plan", "unpermute"]
+           "plan", "unpermute", "get_hadamard", "get_cnot"]
 
 # enum Instruction order (src/circuit.rs:53-68) == enum qdc_kind (include/qdc/circuit.h)
 (CONST_Q2, VAR_Q2, CONST_Q2_NONU, VAR_Q2_NONU, CONST_Q2_DIAG, VAR_Q2_DIAG, CONST_Q1,
@@ -407,6 +408,45 @@ def spec_selftest(tile_bits, stages, deps=None, precision="f32"):
     name = raw.split(b"\0", 1)[0].decode()
     path = raw[len(name) + 1:].split(b"\0", 1)[0].decode()
     return name, path
+
+
+def jit_stats(precision=None):
+    """This process's specialized-kernel cache (qdc_jit_stats): kernels compiled here, kernels
+    waited for while another process compiled them, (kernel, device) loads, seconds compiling,
+    waiting and in the cache overall, whether specialization is on, and launches of specialized
+    kernels."""
+    lib = load(precision or default_precision())
+    v = (C.c_double * 8)()
+    k = int(lib.qdc_jit_stats(v, 8))
+    keys = ("compiled", "waited", "loaded", "compile_s", "wait_s", "total_s", "enabled", "launched")
+    out = {key: float(v[i]) for i, key in enumerate(keys[:k])}
+    for key in ("compiled", "waited", "loaded", "launched"):
+        out[key] = int(out[key])
+    out["enabled"] = bool(out["enabled"])
+    return out
+
+
+def jit_dir(precision=None):
+    """The specialized-kernel cache directory in use; RuntimeError when specialization is off."""
+    lib = load(precision or default_precision())
+    out = C.create_string_buffer(4096)
+    err = lib.qdc_jit_dir(out, 4096)
+    if err:
+        raise RuntimeError(err.decode())
+    return out.value.decode()
+
+
+def spec_fingerprint(csrc_dir, compiler, defines=None, precision="f32"):
+    """(build fingerprint, header hash) a library with `defines` (None: this library's own -D
+    switches), compiler identity text `compiler` and the kernel headers of csrc_dir would name
+    its specialized kernels with (qdc_spec_fingerprint)."""
+    lib = load(precision)
+    fp, sh = C.c_ulonglong(), C.c_ulonglong()
+    err = lib.qdc_spec_fingerprint(None if defines is None else defines.encode(), compiler.encode(),
+                                   str(csrc_dir).encode(), C.byref(fp), C.byref(sh))
+    if err:
+        raise RuntimeError(err.decode())
+    return int(fp.value), int(sh.value)
 
 
 # ---------------------------------------------------------------------------------------

@@ -228,6 +228,25 @@ const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const u
 int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int two_states,
                   int far_tile, unsigned* out);
 
+/* The specialized-kernel cache of this process (qdc_jit.hpp).  stats[0..7] (up to n) =
+ * {kernels compiled by this process, kernels waited for while another process compiled them,
+ * (kernel, device) loads, seconds compiling, seconds waiting, seconds in the cache overall
+ * (compile + wait + load), 1 if specialization is on else 0, launches of specialized kernels}.
+ * Returns the values written. */
+size_t qdc_jit_stats(double* stats, size_t n);
+
+/* The cache directory in use (dir_out, cap >= 2): NULL, or an error message when
+ * specialization is off (no hipcc, kernel headers changed since the build, no private
+ * directory). */
+const char* qdc_jit_dir(char* dir_out, size_t cap);
+
+/* Test hook (host only): the build fingerprint a library with the given -D switches (NULL: this
+ * library's own), compiler identity text and kernel headers (the .hpp files of csrc_dir plus
+ * the .h files of csrc_dir/../../include/qdc) would name its kernels with (qdc_jit.hpp), and
+ * the header hash alone.  Returns NULL, or an error message. */
+const char* qdc_spec_fingerprint(const char* defines, const char* compiler, const char* csrc_dir,
+                                 unsigned long long* fingerprint, unsigned long long* source_hash);
+
 #ifdef __cplusplus
 }
 #endif

@@ -102,9 +102,9 @@ def test_finite_difference_identity():
 def test_ghz_circuit(prec):
     """test_ghz.py:16-60 with the qdc wiring (numpy VJP driver in place of JAX)."""
     from qdc import AutoGradCircuit
+    from quantum_differentiable_circuit.common_gates import get_cnot, get_hadamard
     n = 21
-    cnot = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0], DT[prec])
-    h = (np.array([1, 1, 1, -1]) / np.sqrt(2)).astype(DT[prec])
+    cnot, h = get_cnot(prec), get_hadamard(prec)  # common_gates.rs:19-34
     c = AutoGradCircuit(n, precision=prec)
     c.add_q1_const_gate(0)
     for i in range(n - 1):

@@ -9,6 +9,7 @@ stay within 4x the measured floor of the reference's own algorithm on the same c
 random circuits over every gate kind, on arbitrary qubit pairs (row bits of the tile), with
 densities between the groups; two HIP runs of one circuit differ by at most 8x the floor."""
 import os
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -344,8 +345,14 @@ def test_specialized_passes_equal_interpreted(prec, case):
         c = build_env(prec, n, ins, {"QDC_SPEC": mode, "QDC_SPEC_MAX": 400})
         if psi0 is not None:
             c.set_state_from_vector(fl.psi0)
+        launched = q.jit_stats(prec)["launched"]
         d = c.forward(fl.const, fl.var)
         g = c.backward(fl.cots, fl.const, fl.var)
+        c.synchronize()
+        ran = q.jit_stats(prec)["launched"] - launched
+        # the forced mode really ran specialized kernels (a failed compile would fall back to
+        # the interpreted ones and make this comparison vacuous); mode 0 none
+        assert (ran > 0) == (mode == "2"), (mode, ran, q.jit_stats(prec))
         flat = lambda xs: np.concatenate([np.asarray(x).reshape(-1) for x in xs])
         out[mode] = (flat(d), flat(g), np.asarray(c.get_state(0)), np.asarray(c.get_state(2)))
         what = f"{prec} {case} spec={mode} "
@@ -364,3 +371,60 @@ def test_specialized_passes_equal_interpreted(prec, case):
             print(f"[spec] {prec} {case} {name}: relative difference {rel:.2e}")
             assert rel <= 1e-14, f"{prec} {case}: specialized {name} differ by {rel:.2e}"
     print(f"[spec] {prec} {case}: specialized passes match the interpreted kernels")
+
+
+ABL_LIB = Path(__file__).resolve().parent.parent / "differentiable-quantum-circuit-cuda_amd" / "lib-abl"
+
+
+@pytest.mark.skipif(not (ABL_LIB / "libqdc_f32.so").exists(), reason="ablation build not built")
+def test_ablation_library_kernels_never_reach_production(tmp_path):
+    """The timing-only ablation library (csrc/Makefile `abl`, QDC_RQ_ABL=1: no stage math, wrong
+    results) runs a circuit with specialized passes into a cache directory; the production
+    library then runs the same circuit against the same directory.  The build fingerprint in
+    the kernel names (qdc_jit.hpp) keeps the ablation kernels out: the production process
+    compiles and launches its own, and its results are within the oracle's floors."""
+    import json
+    import subprocess
+    import sys
+    n = 14
+    ins, var = O.layered_circuit(n, 3, seed=51)
+    fl = F.Floor("f32", n, ins, [], var, run=False)
+    np.save(tmp_path / "cots.npy", np.stack([np.asarray(x).reshape(-1) for x in fl.cots]))
+    root = Path(__file__).resolve().parent.parent
+    code = f"""
+import json, sys
+import numpy as np
+sys.path[:0] = [{str(root)!r}, {str(root / 'differentiable-quantum-circuit-cuda_amd')!r}]
+import quantum_differentiable_circuit as q
+from oracle import oracle as O
+ins, var = O.layered_circuit({n}, 3, seed=51)
+c = q.circuit_class("f32")({n})
+for kind, pos in ins:
+    c._push(kind, *pos)
+vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
+d = c.forward([], vg)
+cots = [np.ascontiguousarray(x.reshape(2, 2)) for x in np.load({str(tmp_path / 'cots.npy')!r})]
+g = c.backward(cots, [], vg)
+c.synchronize()
+np.save(sys.argv[1] + "_d.npy", np.concatenate([np.asarray(x).reshape(-1) for x in d]))
+np.save(sys.argv[1] + "_g.npy", np.concatenate([np.asarray(x).reshape(-1) for x in g]))
+print(json.dumps(q.jit_stats("f32")))
+"""
+    (tmp_path / "jit").mkdir(mode=0o700)
+    stats = {}
+    for tag, libdir in (("abl", ABL_LIB), ("prod", None)):
+        env = dict(os.environ, QDC_SPEC="2", QDC_JIT_DIR=str(tmp_path / "jit"))
+        env.pop("QDC_LIB_DIR", None)
+        if libdir is not None:
+            env["QDC_LIB_DIR"] = str(libdir)
+        r = subprocess.run([sys.executable, "-c", code, str(tmp_path / tag)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        stats[tag] = json.loads(r.stdout.strip().splitlines()[-1])
+        print(f"[abl] {tag}: {stats[tag]}")
+    for tag in ("abl", "prod"):
+        assert stats[tag]["enabled"] and stats[tag]["compiled"] > 0 and stats[tag]["launched"] > 0
+    fl.check("forward", np.load(tmp_path / "prod_d.npy"), "ablation-then-production ")
+    grads = np.load(tmp_path / "prod_g.npy")
+    fl.check("grads", grads, "ablation-then-production ")
+    assert F.normrel(np.load(tmp_path / "abl_g.npy"), grads) > 1e-3, "the ablation build computed real gradients"

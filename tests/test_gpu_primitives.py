@@ -107,9 +107,9 @@ def test_q2gate_diag(prec):
 def test_ghz(prec):
     """quantized_tensor.rs:487-506 and the CHECK binary's ghz_test (primitives.cu:961-1033)."""
     q = qt(prec)
+    from quantum_differentiable_circuit.common_gates import get_cnot, get_hadamard
     n = 21
-    h = (np.array([1, 1, 1, -1]) / np.sqrt(2)).astype(DT[prec])
-    cnot = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0], DT[prec])
+    h, cnot = get_hadamard(prec), get_cnot(prec)  # common_gates.rs:19-34
     cz = np.array([1, 1, 1, -1], DT[prec])
     vm = q.QuantizedTensor.new_standard(n, prec)
     vm.apply_q1_gate(h, 0)

@@ -249,8 +249,12 @@ def test_specialized_passes_sharded(prec, kw):
                 del os.environ["QDC_SPEC"]
             else:
                 os.environ["QDC_SPEC"] = old
+        launched = q.jit_stats(prec)["launched"]
         d = c.forward([], fl.var)
         g = c.backward(fl.cots, [], fl.var)
+        c.synchronize()
+        ran = q.jit_stats(prec)["launched"] - launched
+        assert (ran > 0) == (mode == "2"), (mode, ran, q.jit_stats(prec))
         what = f"C2 n={n} {prec} {kw} spec={mode} "
         fl.check("forward", d, what)
         fl.check("grads", g, what)

@@ -67,3 +67,27 @@ def test_state_vector_input(autograd):
     _, run = c.build()
     (rho,) = run([np.eye(2, dtype=np.complex128).reshape(-1)], [])
     assert np.allclose(rho, [[0, 0], [0, 1]])
+
+
+@pytest.mark.parametrize("prec,dt,rt", [("f32", np.complex64, np.float32), ("f64", np.complex128, np.float64)])
+def test_common_gates(prec, dt, rt):
+    """get_hadamard / get_cnot (src/common_gates.rs:19-34) in the build's dtype: row-major,
+    1/sqrt(2) formed in the build's float type, CNOT controlled by pos2 (the local MSB)."""
+    import quantum_differentiable_circuit as q
+    h, cx = q.get_hadamard(prec), q.get_cnot(prec)
+    assert h.dtype == dt and cx.dtype == dt and h.shape == (4,) and cx.shape == (16,)
+    s = rt(1) / np.sqrt(rt(2))
+    assert np.array_equal(h, np.array([s, s, s, -s], dt))
+    u = cx.reshape(4, 4)
+    assert np.array_equal(u @ u, np.eye(4)) and np.array_equal(u[2:, 2:], [[0, 1], [1, 0]])
+    hh = h.astype(np.complex128).reshape(2, 2)
+    assert np.abs(hh @ hh - np.eye(2)).max() < (1e-6 if prec == "f32" else 1e-15)
+    # the GHZ known answer of the reference (primitives.cu:961-1033) through the oracle
+    from oracle import oracle as O
+    n = 6
+    st = np.zeros(1 << n, np.complex128)
+    st[0] = 1
+    st = O.apply_q1_gate(st, h.astype(np.complex128), 0)
+    for i in range(n - 1):
+        st = O.apply_q2_gate(st, cx.astype(np.complex128), i, i + 1)
+    assert abs(st[0] - s) < 1e-6 and abs(st[-1] - s) < 1e-6 and np.abs(st[1:-1]).max() == 0

@@ -3,9 +3,18 @@ generator and hipcc compile a pass program's straight-line kernel for gfx950 (th
 the same at a circuit's first call, then loads the code object).  Checks that the code object is
 a gfx950 offload bundle, that one program maps to one kernel (the cache key), and that the
 generated kernel keeps the interpreted kernel's resources (<= 256 VGPRs, 2 waves/SIMD) without
-its per-stage register copies.  Parity on the GPU: tests/test_gpu_fusion.py."""
+its per-stage register copies.  The cache: kernel names carry the build fingerprint (-D
+switches, compiler, header bytes), so an ablation build, a touched header or another compiler
+never load another build's code object; objects are validated before use; the directory must
+be private; and the processes of a job compile each kernel once.  Parity on the GPU:
+tests/test_gpu_fusion.py."""
+import json
 import os
+import shutil
 import subprocess
+import sys
+import textwrap
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -15,9 +24,35 @@ from test_rq_plan import random_pass
 pytestmark = pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
 
 
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "differentiable-quantum-circuit-cuda_amd"
+HDR = 40  # qdc_jit.hpp JitObjHeader in front of hipcc's output
+
+
 @pytest.fixture(autouse=True)
 def jit_dir(tmp_path, monkeypatch):
     monkeypatch.setenv("QDC_JIT_DIR", str(tmp_path))
+    monkeypatch.setenv("QDC_JIT_KEEP", "1")  # the tests read the generated sources back
+
+
+def _payload(obj, tmp_path):
+    """hipcc's output inside a cached code object (behind the 40-byte header)"""
+    raw = Path(obj).read_bytes()
+    assert raw[:8] == b"QDCJIT2\0", raw[:8]
+    out = tmp_path / "payload.hsaco"
+    out.write_bytes(raw[HDR:])
+    return str(out)
+
+
+def _run(code, env=None, timeout=300):
+    """a fresh process (its own SpecJit state) running `code`; returns its last stdout line as JSON"""
+    e = dict(os.environ)
+    e.update(env or {})
+    pre = (f"import sys, json; sys.path[:0] = [{str(ROOT)!r}, {str(PKG)!r}, {str(ROOT / 'tests')!r}]\n")
+    r = subprocess.run([sys.executable, "-c", pre + textwrap.dedent(code)], env=e,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
 
 
 def _passes(seed, count):
@@ -29,13 +64,13 @@ def _passes(seed, count):
     return out
 
 
-def test_spec_kernel_compiles_for_gfx950_and_is_keyed_by_program():
+def test_spec_kernel_compiles_for_gfx950_and_is_keyed_by_program(tmp_path):
     import quantum_differentiable_circuit as q
     (st1, d1), (st2, d2) = _passes(3, 2)
     name1, obj1 = q.spec_selftest(11, st1, d1)
     assert name1.startswith("qdc_spec_") and os.path.getsize(obj1) > 10000
     bundle = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
-                             "--input=" + obj1], capture_output=True, text=True)
+                             "--input=" + _payload(obj1, tmp_path)], capture_output=True, text=True)
     assert "gfx950" in bundle.stdout, bundle.stdout + bundle.stderr
     # the same program again: the same kernel (no recompilation); another program: another one
     assert q.spec_selftest(11, st1, d1) == (name1, obj1)
@@ -115,3 +150,178 @@ def test_spec_f64_pass_kernels(tmp_path, tile_bits, prefix):
     body = text[text.index(name + ":"):]
     body = body[:body.index(".Lfunc_end")]
     assert body.count("v_mov_b64") < 32
+
+
+# ------------------------------------------------------------------------------------------
+# the cache: build fingerprint, validated objects, private directory, one compile per kernel
+# ------------------------------------------------------------------------------------------
+def _copy_tree(tmp_path):
+    """csrc + include as they sit next to the library (csrc/../../include)"""
+    dst = tmp_path / "tree"
+    shutil.copytree(PKG / "csrc", dst / "pkg" / "csrc")
+    shutil.copytree(ROOT / "include", dst / "include")
+    return dst / "pkg" / "csrc"
+
+
+def test_fingerprint_covers_defines_compiler_and_headers(tmp_path):
+    """The kernel-name fingerprint changes with any -D switch the library was built with
+    (QDC_RQ_ABL: a timing-only build), the compiler identity, and any byte of a kernel header;
+    the header hash equals the one the Makefile compiles in (csrc/src_fp.py)."""
+    import quantum_differentiable_circuit as q
+    r = subprocess.run([sys.executable, str(PKG / "csrc" / "src_fp.py"), str(PKG / "csrc"),
+                        str(ROOT / "include")], capture_output=True, text=True, check=True)
+    assert int(r.stdout, 16) == q.spec_fingerprint(PKG / "csrc", "x")[1]
+    csrc = _copy_tree(tmp_path)
+    own, sh = q.spec_fingerprint(csrc, "hipcc A")  # this library's own -D switches
+    assert q.spec_fingerprint(csrc, "hipcc A") == (own, sh)
+    defs = ("-DQDC_DYN_TAIL=1 -DQDC_FMAX_OPS=40 -DQDC_FMAX_GRAD_RQ=16 -DQDC_RQ_PF_WAVES=2 "
+            "-DQDC_RW_WAVES=2 -DQDC_RW_WAVES_ONE=2 -DQDC_RQ_ABL=0 -DQDC_RQ_GSPLIT=0")
+    abl = defs.replace("QDC_RQ_ABL=0", "QDC_RQ_ABL=1")
+    assert q.spec_fingerprint(csrc, "hipcc A", defines=defs)[0] != \
+        q.spec_fingerprint(csrc, "hipcc A", defines=abl)[0]
+    assert q.spec_fingerprint(csrc, "hipcc B")[0] != own
+    hdr = csrc / "qdc_rq.hpp"
+    hdr.write_text(hdr.read_text() + "\n// touched\n")
+    fp2, sh2 = q.spec_fingerprint(csrc, "hipcc A")
+    assert sh2 != sh and fp2 != own
+    inc = csrc.parent.parent / "include" / "qdc" / "circuit.h"
+    inc.write_text(inc.read_text() + "\n")
+    assert q.spec_fingerprint(csrc, "hipcc A")[1] not in (sh, sh2)
+
+
+ABL_LIB = PKG / "lib-abl" / "libqdc_f32.so"
+
+
+@pytest.mark.skipif(not ABL_LIB.exists(), reason="ablation build (make -C csrc abl) not built")
+def test_ablation_build_never_shares_kernels(tmp_path):
+    """Two builds that differ only in -DQDC_RQ_ABL (the production library and the timing-only
+    ablation library, csrc/Makefile `abl`) compile the same pass program into differently named
+    code objects in one QDC_JIT_DIR, so neither ever loads the other's kernels."""
+    (stages, deps), = _passes(7, 1)
+    out = {}
+    for tag, libdir in (("abl", ABL_LIB.parent), ("prod", PKG / "lib")):
+        out[tag], _ = _run(f"""
+            import quantum_differentiable_circuit as q
+            name, obj = q.spec_selftest(11, {stages!r}, {deps!r})
+            print(json.dumps([name, obj, q.jit_stats('f32')['compiled'], q.jit_dir('f32')]))
+            """, {"QDC_LIB_DIR": str(libdir)})
+    (na, oa, ca, da), (np_, op, cp, dp) = out["abl"], out["prod"]
+    assert da == dp == str(tmp_path)
+    assert na != np_ and oa != op and os.path.exists(oa) and os.path.exists(op)
+    assert ca == 1 and cp == 1  # the production process compiled its own kernel
+
+
+def test_stale_and_corrupt_code_objects_are_rebuilt(tmp_path):
+    """A cached object whose header names another build, or whose bytes are cut short, is never
+    loaded: the next process compiles the kernel again."""
+    (stages, deps), = _passes(8, 1)
+    code = f"""
+        import quantum_differentiable_circuit as q
+        name, obj = q.spec_selftest(11, {stages!r}, {deps!r})
+        print(json.dumps([name, obj, q.jit_stats('f32')['compiled']]))
+        """
+    (name, obj, c1), _ = _run(code)
+    assert c1 == 1
+    (_, _, c2), _ = _run(code)
+    assert c2 == 0  # valid: reused
+    raw = bytearray(Path(obj).read_bytes())
+    raw[8] ^= 0xFF  # the fingerprint of another build
+    Path(obj).write_bytes(bytes(raw))
+    (_, _, c3), _ = _run(code)
+    assert c3 == 1
+    Path(obj).write_bytes(Path(obj).read_bytes()[:-100])  # truncated
+    (_, _, c4), _ = _run(code)
+    assert c4 == 1
+    assert Path(obj).read_bytes()[:8] == b"QDCJIT2\0"
+    # good compiles leave no sources or logs behind (QDC_JIT_KEEP unset)
+    _run(code, {"QDC_JIT_KEEP": "0", "QDC_JIT_DIR": str(tmp_path / "clean")})
+    left = sorted(p.name for p in (tmp_path / "clean").iterdir())
+    assert all(p.endswith((".qco", ".lock")) for p in left), left
+
+
+def test_cache_directory_must_be_private(tmp_path):
+    """QDC_JIT_DIR writable by others, or a symlink, turns specialization off (another user could
+    plant code objects); the default is a 0700 directory under $HOME/.cache."""
+    code = """
+        import quantum_differentiable_circuit as q
+        try:
+            d = q.jit_dir('f32')
+        except RuntimeError as e:
+            d = 'off: ' + str(e)
+        print(json.dumps(d))
+        """
+    open_dir = tmp_path / "open"
+    open_dir.mkdir()
+    open_dir.chmod(0o777)
+    d, err = _run(code, {"QDC_JIT_DIR": str(open_dir)})
+    assert d.startswith("off") and "writable by other users" in err
+    real = tmp_path / "real"
+    real.mkdir(mode=0o700)
+    link = tmp_path / "link"
+    link.symlink_to(real)
+    d, err = _run(code, {"QDC_JIT_DIR": str(link)})
+    assert d.startswith("off") and "not a directory" in err
+    home = tmp_path / "home"
+    home.mkdir(mode=0o700)
+    env = {"HOME": str(home), "XDG_CACHE_HOME": ""}
+    e = dict(os.environ)
+    e.pop("QDC_JIT_DIR", None)
+    os.environ.pop("QDC_JIT_DIR", None)
+    try:
+        d, _ = _run(code, env)
+    finally:
+        os.environ["QDC_JIT_DIR"] = str(tmp_path)
+    assert d == str(home / ".cache" / "qdc_jit")
+    assert (os.stat(d).st_mode & 0o777) == 0o700
+
+
+def test_touched_headers_turn_specialization_off(tmp_path):
+    """Kernel headers that are not the ones the library was built from (QDC_SRC_FP) would
+    compile kernels that disagree with the library's host code: specialization turns off."""
+    csrc = _copy_tree(tmp_path)
+    hdr = csrc / "qdc_spec.hpp"
+    hdr.write_text(hdr.read_text() + "\n// touched\n")
+    (stages, deps), = _passes(9, 1)
+    d, err = _run(f"""
+        import quantum_differentiable_circuit as q
+        try:
+            q.spec_selftest(11, {stages!r}, {deps!r})
+            print(json.dumps("compiled"))
+        except RuntimeError as e:
+            print(json.dumps("off: " + str(e)))
+        """, {"QDC_SRC_DIR": str(csrc)})
+    assert d.startswith("off") and "not the ones this library was built from" in err
+
+
+def test_processes_of_a_job_compile_each_kernel_once(tmp_path):
+    """Four processes sharing one cache directory (the ranks of a multi-process job) ask for the
+    same kernels at the same moment: every kernel is compiled by exactly one of them (a
+    per-kernel lock), the others wait for it and use its code object."""
+    progs = _passes(10, 4)
+    go = tmp_path / "go"
+    code = f"""
+        import os, time
+        import quantum_differentiable_circuit as q
+        while not os.path.exists({str(go)!r}):
+            time.sleep(0.01)
+        names = [q.spec_selftest(11, st, dp)[0] for st, dp in {[(s, d) for s, d in progs]!r}]
+        s = q.jit_stats('f32')
+        print(json.dumps([names, s['compiled'], s['waited']]))
+        """
+    e = dict(os.environ, QDC_JIT_KEEP="0")
+    pre = (f"import sys, json; sys.path[:0] = [{str(ROOT)!r}, {str(PKG)!r}]\n")
+    procs = [subprocess.Popen([sys.executable, "-c", pre + textwrap.dedent(code)], env=e,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for _ in range(4)]
+    import time
+    time.sleep(1.5)  # every process imported and is polling
+    go.write_text("")
+    res = []
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, out + err
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    names = {tuple(r[0]) for r in res}
+    assert len(names) == 1 and len(set(next(iter(names)))) == 4
+    assert sum(r[1] for r in res) == 4, res  # each kernel compiled once in the whole job
+    assert sum(r[2] for r in res) >= 1, res  # and someone waited for another's compile
