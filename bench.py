@@ -53,10 +53,9 @@ def parse():
                     help="rehearse the single-process multi-GPU path on one GPU: G shards, each "
                          "on its own stream of device 0 (event-ordered copies in place of RCCL)")
     ap.add_argument("--no-gate-sample", action="store_true",
-                    help="skip the single-gate (fusion off) kernel sample")
-    ap.add_argument("--cpu-gates", type=int, default=12,
-                    help="gates of the CPU baseline sample (the workload's first gates, full n)")
-    ap.add_argument("--cpu-densities", type=int, default=4)
+                    help="skip the single-gate (fusion off) kernel sweep and the other auxiliary samples")
+    ap.add_argument("--cpu-layers", type=int, default=2,
+                    help="layers of the C2 circuit the CPU baseline runs as one whole call")
     ap.add_argument("--cpu-qubits", type=int, default=None)
     ap.add_argument("--cpu-c3-max-s", type=float, default=120.0,
                     help="time one whole C3 call on the CPU when its projection is below this")
@@ -197,20 +196,24 @@ def _cref_whole_call(ops, n, circuit, dt, psi0=None, cot=None):
 
 
 def cpu_baseline(args, n):
-    """The reference's algorithm on the host cores (oracle/cpu_ref.c: its CUDA kernels'
-    index rules in C/OpenMP, driven in circuit.rs's order: unfused, one kernel per step, a new
-    state per density injection).  Per gate kind, the fwd + bwd cost is timed on full-size
-    states at sampled positions, and projected onto the workload's gate mix:
-      C2 (the headline workload, n = 28 f32): 560 q1 + 540 q2 gates + 28 q1 densities per step,
-        at all threads (OMP default) and at 1 thread (fewer samples);
-      C3 (example_vqse_ising.py, n = 26 f64): 26 layers x (26 diagonal + 26 q1) + 26 q2
-        densities per loss + gradient call, at all threads.
-    value = C2 gate applications per second (fwd + bwd) at all threads."""
+    """The reference's algorithm on the host cores (oracle/cpu_ref.c: its CUDA kernels' index
+    rules in C/OpenMP, driven in circuit.rs's order by oracle.OracleCircuit: unfused, one kernel
+    per step, uncompute + gradient + pull-back per gate backward, a new state per density
+    injection), timed end to end on whole calls:
+      value: one whole forward + backward call of the C2 generator at full n with
+        --cpu-layers layers (default 2: 110 gates) and all of C2's densities, at all threads;
+      full_step: the 20-layer step extrapolated from two measured whole calls (1 and
+        --cpu-layers layers: per-layer slope + the fixed density part), a cross-check;
+      projection: the per-kind fwd+bwd costs (q1 / q2 / density + injection) timed at sampled
+        positions and projected onto the step's gate mix (how earlier rounds reported it);
+      single_thread: the per-kind projection at one thread (a whole call would take minutes);
+      c3_vqse: one whole C3 loss-and-gradient call (n = 26 f64) when its projection is short."""
     # idle OpenMP threads sleep instead of spinning: spinning teams were starved on shared
     # hosts (64-100 ms for a 2 ms kernel in this container); read when libgomp loads
     os.environ.setdefault("OMP_WAIT_POLICY", "passive")
     from oracle.cref import CRefOps
     from quantum_differentiable_circuit import workloads as W
+    dt = np.complex64 if args.precision == "f32" else np.complex128
     ins, _ = W.layered_circuit(n, args.layers, args.seed)
     n_q1 = sum(1 for k, _ in ins if k == 8)
     n_q2 = sum(1 for k, _ in ins if k == 1)
@@ -219,16 +222,33 @@ def cpu_baseline(args, n):
     t_all = time.perf_counter()
     ops = CRefOps(args.precision)
     threads = ops.threads()
+    # whole calls, measured (one untimed layer first: OpenMP team start-up, page first touch)
+    _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), dt)
+    lay = max(2, args.cpu_layers)
+    m1 = _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), dt)
+    mL = _cref_whole_call(ops, n, W.layered_circuit(n, lay, args.seed), dt)
+    g1 = sum(1 for k, _ in m1["ins"] if k in (1, 8))
+    gL = sum(1 for k, _ in mL["ins"] if k in (1, 8))
+    slope = (mL["s"] - m1["s"]) / (lay - 1)
+    full = m1["s"] + (args.layers - 1) * slope
+    res["full_step"] = {"s_per_step": round(full, 2), "value": round((n_q1 + n_q2) / full, 4),
+                        "layer_1_call_s": round(m1["s"], 2), f"layer_{lay}_call_s": round(mL["s"], 2),
+                        "per_layer_s": round(slope, 3),
+                        "method": "t(1 layer) + (layers - 1) x [t(L) - t(1)] / (L - 1) over measured whole calls"}
+    # the per-kind projection (earlier rounds' headline), as a cross-check
     spread = [0, n // 2, n - 1]
     c2 = _cref_op_costs(ops, n, spread, [(p + 1, p) for p in spread[:-1]] + [(n - 1, n - 2)],
                         [0, n - 1], [])
     step = n_q1 * c2["q1"] + n_q2 * c2["q2"] + n_d1 * c2["dens1"]
+    res["projection"] = {"s_per_step": round(step, 2), "value": round((n_q1 + n_q2) / step, 4),
+                         "error_vs_full_step": round((step - full) / full, 4),
+                         "per_gate_s": {k: round(v, 4) for k, v in c2.items()}}
     ops.set_threads(1)
     c2s = _cref_op_costs(ops, n, [n // 2], [(n // 2 + 1, n // 2)], [n // 2], [])
     ops.set_threads(threads)
     step1 = n_q1 * c2s["q1"] + n_q2 * c2s["q2"] + n_d1 * c2s["dens1"]
     res["single_thread"] = {"value": round((n_q1 + n_q2) / step1, 4), "cores": 1,
-                            "s_per_step": round(step1, 2),
+                            "s_per_step": round(step1, 2), "kind": "per-kind projection",
                             "per_gate_s": {k: round(v, 4) for k, v in c2s.items()}}
     # C3: the VQSE circuit at the example's size, f64
     n3, layers3 = 26, 26
@@ -236,26 +256,9 @@ def cpu_baseline(args, n):
     c3 = _cref_op_costs(ops64, n3, [0, n3 // 2, n3 - 1], [], [], [(0, 1), (12, 13), (0, n3 - 1)],
                         [(0, 1), (12, 13), (0, n3 - 1)])
     call = layers3 * n3 * (c3["diag"] + c3["q1"]) + n3 * c3["dens2"]
-    res["c3_vqse"] = {"s_per_loss_grad_call": round(call, 2), "qubits": n3, "layers": layers3,
+    res["c3_vqse"] = {"projected_s_per_call": round(call, 2), "qubits": n3, "layers": layers3,
                       "dtype": "c128 (f64)", "cores": ops64.threads(),
                       "per_gate_s": {k: round(v, 4) for k, v in c3.items()}}
-    # validation of the projections: whole calls of the reference algorithm, timed end to end
-    # (oracle.OracleCircuit = circuit.rs:164-429 over the C kernels; one C2 layer with its 28
-    # densities at full n, and one whole C3 loss-and-gradient call when its projection is short)
-    res["measured"] = measured = {}
-    try:
-        m = _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), np.complex64
-                             if args.precision == "f32" else np.complex128)
-        l_q1 = sum(1 for k, _ in m["ins"] if k == 8)
-        l_q2 = sum(1 for k, _ in m["ins"] if k == 1)
-        l_d1 = sum(1 for k, _ in m["ins"] if k == 13)
-        proj = l_q1 * c2["q1"] + l_q2 * c2["q2"] + l_d1 * c2["dens1"]
-        measured["c2_one_layer"] = {
-            "measured_layer_s": round(m["s"], 2), "projected_s": round(proj, 2),
-            "projection_error": round((proj - m["s"]) / m["s"], 4),
-            "gates": l_q1 + l_q2, "densities": l_d1, "qubits": n, "threads": threads}
-    except Exception as e:  # noqa: BLE001
-        measured["c2_one_layer"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if call <= args.cpu_c3_max_s:
         try:
             p = np.random.default_rng(42).normal(size=2 * layers3)
@@ -264,67 +267,53 @@ def cpu_baseline(args, n):
             psi3 = np.full(1 << n3, 1.0 / np.sqrt(1 << n3), np.complex128)
             m3 = _cref_whole_call(ops64, n3, (ins3, gates3), np.complex128, psi0=psi3,
                                   cot=W.tfim_term(1.0).T.conj())
-            res["c3_vqse"].update({"measured_call_s": round(m3["s"], 2),
+            res["c3_vqse"].update({"s_per_loss_grad_call": round(m3["s"], 2),
                                    "projection_error": round((call - m3["s"]) / m3["s"], 4)})
         except Exception as e:  # noqa: BLE001
             res["c3_vqse"]["measured_error"] = f"{type(e).__name__}: {e}"[:300]
     else:
-        res["c3_vqse"]["measured_call_s"] = f"skipped: projected {call:.0f} s > --cpu-c3-max-s"
+        res["c3_vqse"]["s_per_loss_grad_call"] = f"not measured: projected {call:.0f} s > --cpu-c3-max-s"
     wall = time.perf_counter() - t_all
-    return {"value": round((n_q1 + n_q2) / step, 4), "unit": "gate-applications/s (fwd+bwd)",
-            "cores": threads, "kind": "port", "s_per_step": round(step, 2),
-            "per_gate_s": {k: round(v, 4) for k, v in c2.items()},
-            "sample": (f"per-kind fwd+bwd costs of the reference algorithm (oracle/cpu_ref.c, OpenMP, "
-                       f"unfused, circuit.rs order) timed on full n={n} {args.precision} states: q1 at "
-                       f"{len(spread)} positions, q2 at {len(spread)} pairs, q1 density+injection at 2; "
-                       f"projected onto C2's {n_q1} q1 + {n_q2} q2 gates + {n_d1} densities per "
-                       f"step; single_thread: one position per kind; c3_vqse: n=26 f64 diagonal, "
-                       f"q1 and q2-density costs projected onto 26 layers; measured: one whole C2 "
-                       f"layer (its gates and densities, fwd+bwd, circuit.rs order) and one whole "
-                       f"C3 call timed end to end against their projections; {wall:.0f} s of CPU "
-                       f"time"),
+    return {"value": round(gL / mL["s"], 4), "unit": "gate-applications/s (fwd+bwd)",
+            "cores": threads, "kind": "port", "s_per_call": round(mL["s"], 2),
+            "sample": (f"measured: one whole forward + backward call of the C2 generator at full "
+                       f"n={n} {args.precision} with {lay} layers ({gL} gates) and its {n_d1} "
+                       f"densities, the reference's algorithm (oracle/cpu_ref.c kernels in "
+                       f"circuit.rs order: unfused, per-gate uncompute + gradient + pull-back, a "
+                       f"new state per density injection), OpenMP on {threads} threads, timed end "
+                       f"to end; full_step: the {args.layers}-layer step from the 1- and "
+                       f"{lay}-layer calls; projection / single_thread: per-kind costs; "
+                       f"c3_vqse: one whole n=26 f64 VQSE call; {wall:.0f} s of CPU time"),
             **res}
 
 
-def gate_kernel_sample(args, n):
-    """Single-gate kernels (fusion off): the north star's >= 70 % HBM target is on 1- and
-    2-qubit gate application at n=28 f32.  One circuit with q1 / q2 gates at low, middle and
-    high positions (every kernel family), fwd+bwd x3, per-kernel algorithmic GB/s."""
-    import quantum_differentiable_circuit as q
-    dt = np.complex64 if args.precision == "f32" else np.complex128
-    rng = np.random.default_rng(1)
-    os.environ["QDC_FUSE"] = "0"
-    try:
-        c = q.circuit_class(args.precision)(n)
-    finally:
-        os.environ.pop("QDC_FUSE", None)
-    var = []
-    for _ in range(2):
-        for pos in (0, 1, n // 2, n - 1):
-            c.add_q1_var_gate(pos)
-            var.append(np.ascontiguousarray(O_haar(rng, 2), dtype=dt))
-        for pos2, pos1 in ((1, 0), (n - 1, 0), (n // 2 + 1, n // 2), (n - 1, n - 2)):
-            c.add_q2_var_gate(pos2, pos1)
-            var.append(np.ascontiguousarray(O_haar(rng, 4), dtype=dt))
-    c.get_q1_dens_op_with_grad(0)
-    cot = sigma_z_cotangents(1, dt)
-    c.forward([], var)
-    c.backward(cot, [], var)
-    c.profile(True)
-    for _ in range(3):
-        c.forward([], var)
-        c.backward(cot, [], var)
-    stats = c.profile_collect()
-    c.profile(False)
-    del c
-    out = {}
-    for k in ("apply_q1", "apply_q2", "reverse_q1", "reverse_q2"):
-        if k in stats and stats[k]["total_ms"] > 0:
-            gbs = stats[k]["algo_bytes"] / (stats[k]["total_ms"] * 1e-3) / 1e9
-            out[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                      "launches": stats[k]["launches"],
-                      "avg_ms": round(stats[k]["total_ms"] / stats[k]["launches"], 4)}
-    return out
+def gate_kernel_sweep(args, n, verbose=False):
+    """Single-gate kernels (fusion off): the north star's >= 70 % HBM target on 1- and 2-qubit
+    gate application at n=28 f32, over the SURVEY §8(d) sweep: q1 at every position 0..n-1 and
+    q2 (dense and diagonal) at the pairs (0,1), (1,0), (5,20), (26,27), (27,0), (1,2), (3,9),
+    (14,13); per cell the median over 20 fwd+bwd iterations (after 3 warm-ups) of each
+    kernel's per-launch HIP-event time (apply, reverse = uncompute + gradient + pull-back,
+    inject, density).  Returns every cell and the minimum one."""
+    rows = micro(args, n, verbose=verbose)
+    for lab, k, _, ms, gbs in rows:  # every cell on stderr (the JSON line keeps the summary)
+        print(f"[micro] {lab:10s} {k:18s} {ms:8.4f} ms {gbs:8.1f} GB/s {gbs / HBM_PEAK_GBS:6.1%}",
+              file=sys.stderr, flush=True)
+    cells = [{"case": lab, "kernel": k, "ms": round(ms, 4), "GB/s": round(gbs, 1),
+              "frac": round(gbs / HBM_PEAK_GBS, 4)} for lab, k, _, ms, gbs in rows]
+    # the target's cells: gate application and the reverse sweep's per-gate kernel (not the
+    # reductions or the density injection, which are reported beside them)
+    gate = [c for c in cells if c["kernel"].startswith(("apply_", "reverse_"))]
+    worst = min(gate, key=lambda c: c["frac"]) if gate else None
+    per = {}
+    for c in cells:
+        lo, hi = per.get(c["kernel"], (1e9, 0.0))
+        per[c["kernel"]] = (min(lo, c["frac"]), max(hi, c["frac"]))
+    return {"micro_min": worst,
+            "cells": len(gate), "cells_below_70pct": [f"{c['kernel']} {c['case']} {c['frac']:.3f}"
+                                                       for c in gate if c["frac"] < 0.70],
+            "frac_range_by_kernel": {k: [round(lo, 4), round(hi, 4)] for k, (lo, hi) in sorted(per.items())},
+            "method": "median of 20 fwd+bwd iterations after 3 warm-ups, HIP events per launch, "
+                      "fusion off, a fresh circuit per case, n=%d %s" % (n, args.precision)}
 
 
 def dense_gate_sample(args, n):
@@ -446,12 +435,12 @@ def abi_unfused_sample(args, n):
                     "host sync per gradient, a new state per density injection)"}
 
 
-def micro(args):
+def micro(args, n=None, verbose=True):
     """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse
-    (single-gate kernels: fusion off)."""
-    os.environ["QDC_FUSE"] = "0"
+    (single-gate kernels: fusion off).  Returns (case, kernel, launches, median ms, GB/s) rows."""
     import quantum_differentiable_circuit as q
-    n, prec = args.qubits, args.precision
+    n = args.qubits if n is None else n
+    prec = args.precision
     dt = np.complex64 if prec == "f32" else np.complex128
     rng = np.random.default_rng(0)
     rows = []
@@ -459,7 +448,15 @@ def micro(args):
     def run(label, setup):
         """the median over 20 fwd+bwd iterations (after 3 warm-ups) of each
         kernel's per-launch HIP-event time in the iteration."""
-        c = q.circuit_class(prec)(n)
+        old = os.environ.get("QDC_FUSE")
+        os.environ["QDC_FUSE"] = "0"
+        try:
+            c = q.circuit_class(prec)(n)
+        finally:
+            if old is None:
+                os.environ.pop("QDC_FUSE", None)
+            else:
+                os.environ["QDC_FUSE"] = old
         var = setup(c)
         cots = sigma_z_cotangents(1, dt)
         for _ in range(3):
@@ -479,8 +476,9 @@ def micro(args):
             ms = float(np.median([x[0] for x in v]))
             gbs = v[0][1] / (ms * 1e-3) / 1e9
             rows.append((label, k, v[0][2], ms, gbs))
-            print(f"{label:14s} {k:18s} n={v[0][2]:4d} {ms:8.3f} ms {gbs:8.1f} GB/s  "
-                  f"{gbs / HBM_PEAK_GBS:6.1%}  (median of {len(v)})", flush=True)
+            if verbose:
+                print(f"{label:14s} {k:18s} n={v[0][2]:4d} {ms:8.3f} ms {gbs:8.1f} GB/s  "
+                      f"{gbs / HBM_PEAK_GBS:6.1%}  (median of {len(v)})", flush=True)
         del c
 
     reps = 8
@@ -542,10 +540,12 @@ def main():
         b_ops, _ = q.plan(n, shards, instr, 2, start_phys=end, precision=args.precision)
         remaps = sum(o["type"] == "remap" for o in f_ops + b_ops)
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         c.forward([], vg)
         c.backward(cots, [], vg)
     c.synchronize()
+    warmup_s = time.perf_counter() - tw  # includes the specialized kernels' compilation
 
     c.profile(True)
     barrier(comm)
@@ -559,6 +559,25 @@ def main():
     barrier(comm)
     stats = c.profile_collect()
     c.profile(False)
+
+    # per rank: the specialized-kernel cache (compile / wait seconds, kernels compiled by this
+    # rank: one rank compiles each kernel of a job) and the all-to-all time per step, so a first
+    # multi-GPU run separates JIT warm-up and exchange cost from the passes
+    js = q.jit_stats(args.precision)
+    a2a = stats.get("alltoall", {})
+    mine = [js["total_s"], js["compile_s"], js["wait_s"], float(js["compiled"]),
+            a2a.get("total_ms", 0.0) / args.steps, a2a.get("launches", 0) / args.steps, warmup_s]
+    nf = len(mine)
+    per_rank_vals = [mine]
+    if comm is not None and comm.world > 1:
+        vec = [0.0] * (nf * world)
+        vec[nf * rank:nf * rank + nf] = mine
+        allv = comm.allreduce(vec)
+        per_rank_vals = [allv[nf * r:nf * r + nf] for r in range(world)]
+    per_rank = [{"rank": r, "jit_s": round(v[0], 3), "jit_compile_s": round(v[1], 3),
+                 "jit_wait_s": round(v[2], 3), "kernels_compiled": int(v[3]),
+                 "alltoall_ms_per_step": round(v[4], 3), "alltoalls_per_step": v[5],
+                 "warmup_s": round(v[6], 2)} for r, v in enumerate(per_rank_vals)]
 
     elapsed = max_over_ranks(elapsed, comm)
     value = ngates * args.steps / elapsed  # the one sharded circuit's gate applications
@@ -617,7 +636,7 @@ def main():
                 return fn(*a)
             except Exception as e:  # noqa: BLE001
                 return {"error": f"{type(e).__name__}: {e}"[:300]}
-        gate_kernels = aux(gate_kernel_sample, args, n)
+        gate_kernels = aux(gate_kernel_sweep, args, n)
         dense_kernels = aux(dense_gate_sample, args, n)
         vqse = aux(vqse_sample)
         abi = aux(abi_unfused_sample, args, n)
@@ -673,7 +692,9 @@ def main():
                          "algo_flops_per_launch": dom_flops}
                         if dom_flops > 0 else None),
             "kernels": kernels,
+            "ranks": per_rank,
             "effective_gate_bandwidth": effective,
+            "micro_min": (gate_kernels or {}).get("micro_min") if isinstance(gate_kernels, dict) else None,
             "gate_kernels": gate_kernels,
             "dense_gate_kernels": dense_kernels,
             "vqse_c3": vqse,

@@ -123,6 +123,13 @@ inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint3
   const std::string nr = std::to_string(NR);
   for (size_t j = 0; j < steps.size(); ++j) {
     const SpecStep& s = steps[j];
+    // timing-only ablation builds (QDC_RQ_ABL, qdc_kernels.hpp) drop what the interpreted
+    // kernels drop: 1 the stage math, 2 the relayouts, 4 the Gamma accumulation
+    if ((QDC_RQ_ABL & 2) && s.relayout) continue;
+    if ((QDC_RQ_ABL & 1) && !s.relayout) {
+      if (K.two && (s.F.kind & FOP_GAMMA)) ++ri;
+      continue;
+    }
     if (s.relayout && spec_imm()) {
       // LDS index = bit permutation a(): the current layout's thread bits -> 0..TB-1, slots
       // -> TB..
@@ -154,7 +161,7 @@ inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint3
       continue;
     }
     const uint32_t kind = s.F.kind & 7u;
-    const bool gamma = K.two && (s.F.kind & FOP_GAMMA) != 0;
+    const bool gamma = K.two && (s.F.kind & FOP_GAMMA) != 0 && !(QDC_RQ_ABL & 4);
     const uint32_t c = s.F.t1;
     std::string tpl = kind == FK_Q1 ? "rq_q1<" + std::to_string(c)
                                     : std::string(kind == FK_DIAG ? "rq_diag<" : "rq_q2<") +

@@ -5,9 +5,11 @@ The native runtime owns the RCCL communicator (C ABI qdc_comm_*).  Rank 0 create
 a reader never sees a partial id); the other ranks poll for it.  The file is bound to this
 launch twice over: its name carries MASTER_ADDR/MASTER_PORT, the launcher's run id and the
 launcher's process id (the ranks' common parent under torchrun or mpirun), and its contents
-carry rank 0's start time, which a reader accepts only within `skew` seconds of its own start
-— so an id left behind by an earlier launch that died before rank 0 removed it (same name:
-a shell loop relaunching from one parent) is never taken for this launch's.  rank 0 removes it
+carry rank 0's start time, host and process id: a reader accepts an id only when that start
+time is within `skew` seconds of its own start and, on the same host, that rank 0 is still
+alive — so an id left behind by an earlier launch that died before rank 0 removed it (same
+name: a shell loop relaunching from one parent) is never taken for this launch's.  rank 0
+removes any earlier file before it publishes, and removes its own
 once the communicator exists (ncclCommInitRank returns only after every rank has joined, i.e.
 has read it).  The file lives in the node's temporary directory: this bootstrap is single-node
 (QDC_NCCL_ID_FILE may name a shared path for more).  Usage, under any launcher that exports
@@ -60,21 +62,37 @@ def process_start_time() -> float:
 
 
 _ID_LEN = 128
-_FMT = "<d"  # rank 0's start time after the id
+_FMT = "<dq64s"  # after the id: rank 0's start time, process id and host name
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:  # another user's process: exists
+        return True
+    return True
 
 
 def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: float = 120.0,
                 start: float | None = None) -> bytes:
-    """Rank 0 publishes make_id()'s 128 bytes and its start time at `path` (temporary name +
-    rename: never seen partial); every other rank polls for a file whose rank-0 start time is
-    within `skew` s of its own start (ranks of one launch start together; a stale file of an
-    earlier launch is older)."""
+    """Rank 0 publishes make_id()'s 128 bytes, its start time, pid and host at `path` (temporary
+    name + rename: never seen partial); every other rank polls for a file whose rank-0 start
+    time is within `skew` s of its own start (ranks of one launch start together; a stale file
+    of an earlier launch is older) and whose rank 0, if on this host, is alive (a launch that
+    died left its file behind)."""
     path = Path(path)
     start = process_start_time() if start is None else start
+    host = os.uname().nodename.encode()[:64]
     if rank == 0:
+        try:
+            path.unlink()  # an earlier launch's file: gone before this launch's id appears
+        except FileNotFoundError:
+            pass
         raw = make_id()
         tmp = path.with_name(path.name + f".tmp{os.getpid()}")
-        tmp.write_bytes(raw + struct.pack(_FMT, start))
+        tmp.write_bytes(raw + struct.pack(_FMT, start, os.getpid(), host))
         os.replace(tmp, path)
         return raw
     t0 = time.monotonic()
@@ -82,8 +100,9 @@ def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: fl
         try:
             data = path.read_bytes()
             if len(data) == _ID_LEN + struct.calcsize(_FMT):
-                (t_root,) = struct.unpack(_FMT, data[_ID_LEN:])
-                if abs(t_root - start) <= skew:
+                t_root, pid, h = struct.unpack(_FMT, data[_ID_LEN:])
+                live = h.rstrip(b"\0") != host or _alive(pid)
+                if abs(t_root - start) <= skew and live:
                     return data[:_ID_LEN]
         except FileNotFoundError:
             pass

@@ -91,3 +91,30 @@ def test_common_gates(prec, dt, rt):
     for i in range(n - 1):
         st = O.apply_q2_gate(st, cx.astype(np.complex128), i, i + 1)
     assert abs(st[0] - s) < 1e-6 and abs(st[-1] - s) < 1e-6 and np.abs(st[1:-1]).max() == 0
+
+
+def test_rccl_id_bootstrap_ignores_a_dead_launch(tmp_path):
+    """distributed.exchange_id: an id file left by an earlier launch whose rank 0 died is never
+    taken (same name, start time within the skew); rank 0 of this launch replaces it."""
+    import os
+    import struct
+    import subprocess
+    import sys
+    from quantum_differentiable_circuit import distributed as D
+    path = tmp_path / "id"
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    now = D.process_start_time()
+    host = os.uname().nodename.encode()
+    path.write_bytes(b"s" * 128 + struct.pack(D._FMT, now, dead.pid, host))
+    with pytest.raises(TimeoutError):
+        D.exchange_id(1, path, None, timeout=0.3, start=now)
+    # a live rank 0 on another host (a shared id path) is taken on its start time alone
+    path.write_bytes(b"o" * 128 + struct.pack(D._FMT, now, dead.pid, b"elsewhere"))
+    assert D.exchange_id(1, path, None, timeout=1, start=now) == b"o" * 128
+    assert D.exchange_id(0, path, lambda: b"n" * 128, start=now) == b"n" * 128
+    assert D.exchange_id(1, path, None, timeout=1, start=now) == b"n" * 128
+    # an id of a launch that started long before this rank: rejected
+    path.write_bytes(b"x" * 128 + struct.pack(D._FMT, now - 1000, os.getpid(), host))
+    with pytest.raises(TimeoutError):
+        D.exchange_id(1, path, None, timeout=0.3, start=now)
