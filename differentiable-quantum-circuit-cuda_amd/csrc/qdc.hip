@@ -497,11 +497,15 @@ QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds,
   if (n == 0 || n > 64 || !name_out || cap < 128) return "invalid arguments";
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
-  // the runtime's tiles: f32 11 two-state (five slots), 12 one-state; f64 10 two-state, 11 one-state
+  // the runtime's tiles: f32 11 two-state (five slots), 12 one-state; f64 10 two-state, 11 one-state;
+  // tile_bits | 0x100: a one-state pass on the two-state tile size (f32: one wave, five slots)
+  // | 0x200 as well: that pass prefetching the next tile (f32 one-wave: k_rw<false, 2, true, 1, true>)
+  const bool force_one = (tile_bits & 0x100u) != 0, pf = (tile_bits & 0x200u) != 0;
+  tile_bits &= 0xffu;
   const unsigned t2bits = sizeof(qdc::real) == 4 ? 11u : 10u;
   if (tile_bits != t2bits && tile_bits != t2bits + 1) return "tile_bits: not a specialized pass's tile";
-  const bool two = tile_bits == t2bits;
-  const qdc::SpecKind K = two ? qdc::spec_kind_two() : qdc::spec_kind_one(tile_bits);
+  const bool two = tile_bits == t2bits && !force_one;
+  const qdc::SpecKind K = two ? qdc::spec_kind_two() : qdc::spec_kind_one(tile_bits, pf);
   const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, K.ns);
   std::vector<qdc::SpecStep> sst;
   qdc::RqLayout cur = plan.load;

@@ -237,6 +237,9 @@ struct Circuit {
   // instead of four-wave, four-slot k_rq ones (QDC_RQ_FWD5)
   int rq_fwd5 = 0;  // measured 4 % slower per pass (r3i): 16 KiB of LDS per wave caps it at 2 waves/SIMD
   bool rq5() const { return rq_slots5 != 0 && (rq_wave & 1) && !(rq_wave & 4); }
+  // one-state one-wave five-slot passes (2^11 tiles, QDC_RW bit 1) prefetch the next tile
+  // (QDC_RW bit 3, with QDC_RQ_PF)
+  bool rw1_prefetch() const { return (rq_wave & 8) && rq_prefetch; }
   // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
   // XCD-aware block order (QDC_RQ_ORDER)
   int rq_order = 0;
@@ -257,6 +260,9 @@ struct Circuit {
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
   uint32_t rq_perm_low = 0;  // low positions a permuting pass fills, 0: default (QDC_RQ_PERM_LOW)
   int rq_gstage = 1;  // two-state passes capped by Gamma stages, not variable gates (QDC_RQ_GSTAGE)
+  // one-state fused tile in chunks (QDC_TILE1_CHUNKS): TILE_CHUNKS_1, or TILE_CHUNKS_2 (f32: 2^11
+  // amplitudes, one wave per tile on k_rw with five slots when QDC_RW bit 1 is set)
+  uint32_t tile1_chunks = TILE_CHUNKS_1;
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -321,6 +327,12 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
+    if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
+      const uint32_t t = (uint32_t)atoi(e);
+      if (t != TILE_CHUNKS_1 && t != TILE_CHUNKS_2)
+        return fail("QDC_TILE1_CHUNKS must be %u or %u", TILE_CHUNKS_1, TILE_CHUNKS_2);
+      tile1_chunks = t;
+    }
     if (const char* e = getenv("QDC_SPEC")) spec_mode = atoi(e);
     if (const char* e = getenv("QDC_SPEC_MIN_QUBITS")) spec_min_qubits = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_MAX")) spec_max = (uint32_t)atoi(e);
@@ -639,6 +651,7 @@ struct Circuit {
     P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
     P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
+    P.tile1_chunks = tile1_chunks;
     P.gamma_stage_cap = rq_gstage != 0;
     return P;
   }
@@ -984,7 +997,8 @@ struct Circuit {
       // 2^12 tiles; f64 two-state k_rw on 2^10 tiles, one-state on 2^10 / 2^11
       const bool f32 = sizeof(real) == 4;
       const bool spec1 = spec_on() && spec_fwd && !two &&
-                         (f32 ? (!it.s5 && it.tbits == 12 && rq_prefetch && !(rq_wave & 2))
+                         (f32 ? ((!it.s5 && it.tbits == 12 && rq_prefetch && !(rq_wave & 2)) ||
+                                 (it.s5 && it.tbits == 11 && (rq_wave & 2)))
                               : (it.tbits == 10 || it.tbits == 11));
       const bool spec = spec1 || (spec_on() && two && (f32 ? (it.s5 && rq5()) : it.tbits == 10));
       std::vector<SpecStep> sst;
@@ -1031,7 +1045,8 @@ struct Circuit {
       if (spec) {
         // the source is generated once per distinct program (per process): the key is
         // everything it depends on, the layouts, stage kinds, slot cases and Γ flags
-        std::vector<uint32_t> key = {spec1 ? 1u : 2u, it.tbits, spec_imm() ? 1u : 0u};
+        const bool pf1 = spec1 && it.s5 && rw1_prefetch();
+        std::vector<uint32_t> key = {spec1 ? 1u : 2u, it.tbits, spec_imm() ? 1u : 0u, pf1 ? 1u : 0u};
         auto put_layout_key = [&](const RqLayout& L) {
           key.push_back(L.ns | (L.tfix ? 0x100u : 0u));
           for (uint32_t q = 0; q < RQ_SLOTS_MAX; ++q) key.push_back(L.slot[q]);
@@ -1049,7 +1064,7 @@ struct Circuit {
         }
         auto hit = spec_cache.find(key);
         if (hit == spec_cache.end()) {
-          const SpecKind K = spec1 ? spec_kind_one(it.tbits) : spec_kind_two();
+          const SpecKind K = spec1 ? spec_kind_one(it.tbits, pf1) : spec_kind_two();
           const std::string body = spec_program_source(sst, it.tbits, K);
           SpecEntry e;
           e.name = spec_kernel_name(body, K);
@@ -1140,11 +1155,29 @@ struct Circuit {
   const char* launch_fused(Ctx& ctx, const char* name, double bytes, const fgeo& fg, chunk* f,
                            chunk* b, const fop* fops, const cx* mats, cx* partials,
                            uint64_t stride) {
+    // one-state passes on the smaller tile (QDC_TILE1_CHUNKS = TILE_CHUNKS_2): the LDS kernel
+    // of that tile size (a k_fused tile is always TB chunks)
+    if constexpr (!TWO) {
+      if ((1ull << (fg.lc + fg.h)) == TILE_CHUNKS_2)
+        return launch_fused_tb<TWO, HASRED, WF, (int)TILE_CHUNKS_2>(ctx, name, bytes, fg, f, b, fops,
+                                                                    mats, partials, stride);
+    }
+    constexpr int TB = TWO ? (int)TILE_CHUNKS_2 : (int)TILE_CHUNKS_1;
+    return launch_fused_tb<TWO, HASRED, WF, TB>(ctx, name, bytes, fg, f, b, fops, mats, partials, stride);
+  }
+  template <bool TWO, bool HASRED, bool WF, int TB>
+  const char* launch_fused_tb(Ctx& ctx, const char* name, double bytes, const fgeo& fg, chunk* f,
+                              chunk* b, const fop* fops, const cx* mats, cx* partials,
+                              uint64_t stride) {
+    if ((1ull << (fg.lc + fg.h)) != (uint64_t)TB)
+      return fail("internal: a %llu-chunk fused tile on the %d-chunk LDS kernel",
+                  (unsigned long long)(1ull << (fg.lc + fg.h)), TB);
     // 256 threads per tile (measured: 128 threads with twice the quartets per thread and
     // occupancy 2 was 2-4 % slower)
     constexpr int NT = 256;
+    auto kern = k_fused<TWO, TB, HASRED, WF, NT>;
     uint32_t grid = 0;
-    QDC_TRY(fused_grid(fg, (const void*)fused_kernel<TWO, HASRED, WF, NT>(), NT, grid));
+    QDC_TRY(fused_grid(fg, (const void*)kern, NT, grid));
     fgeo g = fg;
     uint64_t tpb = 1;
     while (tpb * grid < g.ntiles) tpb <<= 1;
@@ -1153,8 +1186,8 @@ struct Circuit {
     if (g.ngrad > 0 && grid > NBMAX) return fail("fused reduction grid %u exceeds %u", grid, NBMAX);
     last_fused_grid = grid;
     last_fused_ndyn = 0;
-    return ctx.launch_block(name, bytes, fused_kernel<TWO, HASRED, WF, NT>(), grid, (uint32_t)NT,
-                            f, b, fops, mats, g, partials, stride);
+    return ctx.launch_block(name, bytes, kern, grid, (uint32_t)NT, f, b, fops, mats, g, partials,
+                            stride);
   }
   // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
   const char* launch_rq(Ctx& ctx, const char* name, double bytes, const fgeo& fg, bool two,
@@ -1177,6 +1210,24 @@ struct Circuit {
       last_fused_grid = grid;
       last_fused_ndyn = 0;
       return ctx.launch_block(name, bytes, k_rw<false, 2, true, 2, true>, grid, 128u, f, b, fops,
+                              mats, g, l0, partials, stride);
+    }
+    if (!two && s5 && nt == 128 && rw1_prefetch()) {  // one wave per 2^11 tile, prefetching
+      const void* kw = (const void*)k_rw<false, 2, true, 1, true>;
+      uint32_t grid = 0;
+      QDC_TRY(fused_grid(fg, kw, 64, grid));
+      fgeo g = fg;
+      if (!(g.ngrad == 0 && grid >= 8 && g.ntiles >= 4ull * grid && ctx.plan_dyn(g, grid))) {
+        uint64_t tpb = 1;
+        while (tpb * grid < g.ntiles) tpb <<= 1;
+        g.tpb = (uint32_t)tpb;
+        grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+      }
+      last_fused_grid = grid;
+      last_fused_ndyn = 0;
+      if (spec)
+        return ctx.launch_module(name, bytes, spec, grid, 64u, f, b, fops, mats, g, l0, partials, stride);
+      return ctx.launch_block(name, bytes, k_rw<false, 2, true, 1, true>, grid, 64u, f, b, fops,
                               mats, g, l0, partials, stride);
     }
     if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
@@ -1216,6 +1267,9 @@ struct Circuit {
       if (two)
         return ctx.launch_block(name, bytes, k_rw<true, 2, false, 1>, grid, bs, f, b, fops, mats, g,
                                 l0, partials, stride);
+      if (nt == 128 && s5 && spec)  // one-wave one-state pass, specialized
+        return ctx.launch_module(name, bytes, spec, grid, bs, f, b, fops, mats, g, l0, partials,
+                                 stride);
       if (nt == 128 && s5)
         return ctx.launch_block(name, bytes, k_rw<false, 2, false, 1, true>, grid, bs, f, b, fops,
                                 mats, g, l0, partials, stride);

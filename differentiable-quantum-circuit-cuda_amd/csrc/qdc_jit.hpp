@@ -85,8 +85,16 @@ inline SpecKind spec_kind_two() {
   return {true, 6, 5, false, "qdc_spec_", "qdc::rw_pass<true, 2, false, 1, true, Prog>", 64,
           "QDC_RW_WAVES, QDC_RW_WAVES"};
 }
-// k_rq<false, 256, true>: f32 one-state, four waves, prefetching
-inline SpecKind spec_kind_one(uint32_t) {
+// k_rq<false, 256, true>: f32 one-state 2^12 tiles, four waves, prefetching; k_rw<false, 2,
+// false, 1, true>: 2^11 tiles (QDC_TILE1_CHUNKS=1024, QDC_RW bit 1), one wave, five slots
+// (pf: the next tile prefetched into pinned VGPRs, k_rw<false, 2, true, 1, true>, QDC_RW bit 3)
+inline SpecKind spec_kind_one(uint32_t T, bool pf = false) {
+  if (T == 11 && pf)
+    return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, true, 1, true, Prog>", 64,
+            "QDC_RW_WAVES, QDC_RW_WAVES"};
+  if (T == 11)
+    return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, false, 1, true, Prog>", 64,
+            "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};
   return {false, 8, 4, true, "qdc_specf_", "qdc::rq_pass<false, 256, true, Prog>", 256,
           "QDC_RQ_PF_WAVES"};
 }
@@ -97,7 +105,7 @@ inline SpecKind spec_kind_two() {
           "QDC_RW_WAVES, QDC_RW_WAVES"};
 }
 // k_rw<false, 1, false, W>: f64 one-state, W = 1 (2^10 tiles) or 2 (2^11)
-inline SpecKind spec_kind_one(uint32_t T) {
+inline SpecKind spec_kind_one(uint32_t T, bool = false) {
   if (T == 10)
     return {false, 6, 4, false, "qdc_specf_d_", "qdc::rw_pass<false, 1, false, 1, false, Prog>", 64,
             "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};

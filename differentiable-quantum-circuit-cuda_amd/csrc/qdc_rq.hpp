@@ -730,8 +730,8 @@ __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict
                                         fgeo fg, uint32_t l0, cx* __restrict__ partials,
                                         uint64_t slot_stride) {
   static_assert(NE == 1 || NE == 2 || NE == 4, "k_rw: 1, 2 or 4 register groups");
-  static_assert(!S5 || (NE == 2 && VEC == 2 && ((W == 1 && !PF) || (W == 2 && PF && !TWO))),
-                "five slots: f32 one-wave tiles, or the two-wave prefetching one-state tiles");
+  static_assert(!S5 || (NE == 2 && VEC == 2 && ((W == 1 && (!PF || !TWO)) || (W == 2 && PF && !TWO))),
+                "five slots: f32 one-wave tiles, or the prefetching one-state tiles");
   static_assert(W == 1 || (W == 2 && !TWO), "k_rw: two-state tiles are one wave");
   constexpr int LOGNE = NE == 1 ? 0 : NE == 2 ? 1 : 2;
   constexpr int TB = W == 1 ? 6 : 7;  // k_rq thread bits held by the block's threads
@@ -873,7 +873,7 @@ __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict
   };
   auto run = [&](cx (&xf)[R], cx (&xb)[R]) __attribute__((always_inline)) {
     if constexpr (!std::is_same<PROG, void>::value) {
-      static_assert(!PF, "specialized k_rw passes: non-prefetching instances");
+      static_assert(!PF || !TWO, "specialized k_rw passes: no two-state prefetching instance");
       const SpecEnv E{mats, ops, accw, lane, bufb};
       if constexpr (TWO)
         PROG{}(xf, xb, E);
@@ -965,10 +965,11 @@ __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict
       tile(t);
     }
   } else if constexpr (!TWO) {
-    // one-state prefetch (W = 2, NE = 2, S5): this lane's 16 chunks of the next tile in flight in
+    // one-state prefetch (W = 1 or 2, NE = 2, S5): this lane's 16 chunks of the next tile in flight in
     // pinned v[192:255] while this tile runs; step s takes tile s-1, issues tile s, runs and
     // stores tile s-1 (k_rq's PF loop, with k_rw's register groups)
-    static_assert(NE == 2 && W == 2 && S5 && CPT == 16, "one-state prefetch: 2^12 S5 tiles");
+    static_assert(NE == 2 && (W == 1 || W == 2) && S5 && CPT == 16,
+                  "one-state prefetch: S5 tiles of 2^11 (one wave) or 2^12 (two waves) amplitudes");
     constexpr int NLD = CPT;  // vector-memory ops per tile: loads = stores
     vec16 pf_a[8], pf_b[8];   // chunks 0..7 (register group 0) and 8..15 (group 1)
     auto issue = [&](uint64_t base) __attribute__((always_inline)) {

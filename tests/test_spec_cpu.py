@@ -325,3 +325,28 @@ def test_processes_of_a_job_compile_each_kernel_once(tmp_path):
     assert len(names) == 1 and len(set(next(iter(names)))) == 4
     assert sum(r[1] for r in res) == 4, res  # each kernel compiled once in the whole job
     assert sum(r[2] for r in res) >= 1, res  # and someone waited for another's compile
+
+
+@pytest.mark.parametrize("pf", [0, 0x200])
+def test_spec_one_wave_forward_pass_kernel(tmp_path, pf):
+    """One-state passes on 2^11 tiles (QDC_TILE1_CHUNKS=1024 with QDC_RW bit 1: k_rw<false, 2,
+    false, 1, true>, one wave, five register slots; with QDC_RW bit 3 the next tile prefetched
+    into pinned VGPRs, k_rw<false, 2, true, 1, true>) written out per program: no scratch,
+    within the two waves per SIMD the generic kernel runs at."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(21)
+    stages, deps = random_pass(rng, 11, 12, brick=True)
+    name, obj = q.spec_selftest(11 | 0x100 | pf, stages, deps)
+    assert name.startswith("qdc_specf_") and os.path.getsize(obj) > 10000
+    src = os.path.join(os.path.dirname(obj), name + "." + str(os.getpid()) + ".hip")
+    csrc = os.path.join(os.path.dirname(q.__file__), "..", "csrc")
+    inc = os.path.join(csrc, "..", "..", "include")
+    asm = tmp_path / "k.s"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "-I" + inc, "-I" + csrc, "-S", "--cuda-device-only", "-o", str(asm), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = asm.read_text()
+    meta = text[text.index(".amdhsa_kernel " + name):]
+    assert int(meta.split(".amdhsa_next_free_vgpr")[1].split()[0]) <= 256
+    assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
