@@ -491,10 +491,11 @@ QDC_API int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1,
 // qdc_rq_plan; a two-state pass's stages all Gamma stages) on the runtime's tile of the
 // precision, write its kernel source and compile it with hipcc for gfx950 (not loaded).  name_out receives the kernel name
 // and, after a NUL, the code object's path.  Returns nullptr or an error message.
-QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
-                                      const unsigned* t2, const unsigned long long* deps, size_t n,
-                                      char* name_out, size_t cap) {
-  if (n == 0 || n > 64 || !name_out || cap < 128) return "invalid arguments";
+// the specialized kernel (name, source) of one pass program over n stages (qdc_spec_selftest)
+static const char* spec_program_for(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+                                    const unsigned* t2, const unsigned long long* deps, size_t n,
+                                    std::string& name, std::string& src) {
+  if (n == 0 || n > 64) return "invalid arguments";
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
   // the runtime's tiles: f32 11 two-state (five slots), 12 one-state; f64 10 two-state, 11 one-state;
@@ -525,12 +526,45 @@ QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds,
     sst.push_back(qdc::SpecStep{false, cur, cur, F});
   }
   const std::string body = qdc::spec_program_source(sst, tile_bits, K);
-  const std::string name = qdc::spec_kernel_name(body, K), src = qdc::spec_kernel_source(name, body, K);
+  name = qdc::spec_kernel_name(body, K);
+  src = qdc::spec_kernel_source(name, body, K);
+  return nullptr;
+}
+
+QDC_API const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
+                                      const unsigned* t2, const unsigned long long* deps, size_t n,
+                                      char* name_out, size_t cap) {
+  if (!name_out || cap < 128) return "invalid arguments";
+  std::string name, src;
+  if (const char* e = spec_program_for(tile_bits, kinds, t1, t2, deps, n, name, src)) return e;
   if (const char* e = qdc::SpecJit::get().compile_only({name}, {src})) return e;
   const std::string obj = qdc::SpecJit::get().code_object(name);
   if (name.size() + obj.size() + 2 > cap) return "name buffer too small";
   std::memcpy(name_out, name.c_str(), name.size() + 1);
   std::memcpy(name_out + name.size() + 1, obj.c_str(), obj.size() + 1);
+  return nullptr;
+}
+
+QDC_API const char* qdc_spec_selftest_batch(unsigned tile_bits, const size_t* counts, size_t nprog,
+                                            const unsigned* kinds, const unsigned* t1,
+                                            const unsigned* t2, const unsigned long long* deps,
+                                            char* names_out, size_t cap) {
+  if (!counts || !names_out || nprog == 0) return "invalid arguments";
+  std::vector<std::string> names(nprog), srcs(nprog);
+  size_t off = 0;
+  for (size_t p = 0; p < nprog; ++p) {
+    if (const char* e = spec_program_for(tile_bits, kinds + off, t1 + off, t2 + off,
+                                         deps ? deps + off : nullptr, counts[p], names[p], srcs[p]))
+      return e;
+    off += counts[p];
+  }
+  if (const char* e = qdc::SpecJit::get().compile_only(names, srcs)) return e;
+  size_t w = 0;
+  for (const std::string& nm : names) {
+    if (w + nm.size() + 1 > cap) return "name buffer too small";
+    std::memcpy(names_out + w, nm.c_str(), nm.size() + 1);
+    w += nm.size() + 1;
+  }
   return nullptr;
 }
 

@@ -572,64 +572,93 @@ class SpecJit {
     struct stat st;
     return stat(p.c_str(), &st) == 0;
   }
-  // The missing kernels `todo`: one process compiles each.  A kernel whose lock this process
-  // takes (flock, released by the kernel if the holder dies) and whose object is still missing
-  // is compiled here, in parallel with the others taken; a kernel another process holds is
-  // waited for, then loaded — or compiled here if that process failed.
+  // compile parallelism of this process: the node's hipcc processes shared by the job's ranks
+  int jobs_now() const {
+    int jobs = std::min((int)std::thread::hardware_concurrency(), 16) / procs;
+    if (const char* e = getenv("QDC_JIT_JOBS")) jobs = atoi(e);
+    return std::max(1, std::min(jobs, 16));
+  }
+  // The missing kernels `todo`: one process compiles each.  Work-stealing over per-kernel locks
+  // (flock, released by the kernel if the holder dies): take up to this process's compile
+  // parallelism of the free locks whose object is still missing, compile them, release, repeat;
+  // when every remaining kernel is held by another process, wait for one, then load it — or
+  // compile it here if that process failed.  So the ranks of a job share the compiles instead of
+  // the first one taking them all.
   bool obtain(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
               const std::vector<size_t>& todo) {
-    std::vector<size_t> mine;
-    std::vector<int> held;
-    std::vector<std::pair<size_t, int>> others;
+    auto lock_fd = [&](size_t i) {
+      return open(lock_path(names[i]).c_str(), O_RDWR | O_CREAT | O_CLOEXEC | O_NOFOLLOW, 0600);
+    };
     auto release = [](int fd) {
       flock(fd, LOCK_UN);
       close(fd);
     };
-    for (size_t i : todo) {
-      const int fd = open(lock_path(names[i]).c_str(), O_RDWR | O_CREAT | O_CLOEXEC | O_NOFOLLOW, 0600);
-      if (fd < 0) {
-        for (int h : held) release(h);
-        for (auto& o : others) close(o.second);
-        disable("cannot create " + lock_path(names[i]));
-        return false;
-      }
-      if (flock(fd, LOCK_EX | LOCK_NB) == 0) {
-        if (image(names[i])) {  // finished by another process meanwhile
+    double wait_lim = 900;
+    if (const char* e = getenv("QDC_JIT_WAIT_S")) wait_lim = atof(e);
+    const int jobs = jobs_now();
+    std::vector<size_t> rem = todo;
+    // start at a process-dependent kernel: concurrent ranks begin on different locks
+    if (!rem.empty()) std::rotate(rem.begin(), rem.begin() + (size_t)getpid() % rem.size(), rem.end());
+    while (!rem.empty()) {
+      std::vector<size_t> batch, left;
+      std::vector<int> held;
+      for (size_t i : rem) {
+        if (image(names[i])) continue;  // done (here or elsewhere)
+        if ((int)batch.size() >= jobs) {
+          left.push_back(i);
+          continue;
+        }
+        const int fd = lock_fd(i);
+        if (fd < 0) {
+          for (int h : held) release(h);
+          disable("cannot create " + lock_path(names[i]));
+          return false;
+        }
+        if (flock(fd, LOCK_EX | LOCK_NB) != 0) {  // another process compiles it
+          close(fd);
+          left.push_back(i);
+          continue;
+        }
+        if (image(names[i])) {  // finished between the check and the lock
           release(fd);
           continue;
         }
-        mine.push_back(i);
+        batch.push_back(i);
         held.push_back(fd);
-      } else {
-        others.emplace_back(i, fd);
       }
-    }
-    bool ok = mine.empty() || compile(names, srcs, mine);
-    for (int h : held) release(h);
-    double wait_lim = 900;
-    if (const char* e = getenv("QDC_JIT_WAIT_S")) wait_lim = atof(e);
-    for (auto& o : others) {
-      if (!ok) {
-        close(o.second);
+      if (!batch.empty()) {
+        const bool ok = compile(names, srcs, batch);
+        for (int h : held) release(h);
+        if (!ok) return false;
+        rem = left;
         continue;
+      }
+      if (left.empty()) break;
+      // every remaining kernel is being compiled elsewhere: wait for the first of them
+      const size_t i = left.front();
+      const int fd = lock_fd(i);
+      if (fd < 0) {
+        disable("cannot create " + lock_path(names[i]));
+        return false;
       }
       const double t0 = now();
       ++stats.waited;
-      while (flock(o.second, LOCK_EX | LOCK_NB) != 0) {
+      while (flock(fd, LOCK_EX | LOCK_NB) != 0) {
         if (now() - t0 > wait_lim) {
-          close(o.second);
-          disable("timed out waiting for another process compiling " + names[o.first]);
-          ok = false;
-          break;
+          close(fd);
+          stats.wait_s += now() - t0;
+          disable("timed out waiting for another process compiling " + names[i]);
+          return false;
         }
         usleep(20000);
       }
       stats.wait_s += now() - t0;
-      if (!ok) continue;
-      if (!image(names[o.first])) ok = compile(names, srcs, {o.first});
-      release(o.second);
+      const bool ok = image(names[i]) || compile(names, srcs, {i});
+      release(fd);
+      if (!ok) return false;
+      rem = left;
     }
-    return ok;
+    return true;
   }
   // write `elf` as the code object of `name` (header + bytes) by atomic rename
   bool publish(const std::string& name, const std::string& elf, const std::string& tag) {
@@ -653,9 +682,7 @@ class SpecJit {
   bool compile(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
                const std::vector<size_t>& todo) {
     const double t0 = now();
-    int jobs = std::min((int)std::thread::hardware_concurrency(), 16) / procs;
-    if (const char* e = getenv("QDC_JIT_JOBS")) jobs = atoi(e);
-    jobs = std::max(1, std::min(jobs, 16));
+    const int jobs = jobs_now();
     const char* keep_env = getenv("QDC_JIT_KEEP");  // keep sources and logs of good compiles
     const bool keep = keep_env && atoi(keep_env) != 0;
     struct Job {

@@ -410,6 +410,27 @@ def spec_selftest(tile_bits, stages, deps=None, precision="f32"):
     return name, path
 
 
+def spec_selftest_batch(tile_bits, programs, precision="f32"):
+    """spec_selftest for several pass programs [(stages, deps), ...] compiled in one call of the
+    kernel cache (qdc_spec_selftest_batch), as a circuit call compiles its missing kernels.
+    Returns the kernel names."""
+    lib = load(precision)
+    counts = (C.c_size_t * len(programs))(*[len(st) for st, _ in programs])
+    flat = [s for st, _ in programs for s in st]
+    dflat = [int(d) for st, dp in programs for d in (dp or [0] * len(st))]
+    n = len(flat)
+    kinds = (C.c_uint * n)(*[int(s[0]) for s in flat])
+    t1 = (C.c_uint * n)(*[int(s[1]) for s in flat])
+    t2 = (C.c_uint * n)(*[int(s[2]) for s in flat])
+    dp = (C.c_ulonglong * n)(*dflat)
+    out = C.create_string_buffer(64 * len(programs) + 16)
+    err = lib.qdc_spec_selftest_batch(tile_bits, counts, len(programs), kinds, t1, t2, dp, out,
+                                      len(out))
+    if err:
+        raise RuntimeError(err.decode())
+    return [x.decode() for x in out.raw.split(b"\0")[:len(programs)]]
+
+
 def jit_stats(precision=None):
     """This process's specialized-kernel cache (qdc_jit_stats): kernels compiled here, kernels
     waited for while another process compiled them, (kernel, device) loads, seconds compiling,

@@ -35,7 +35,7 @@ RUNTIME = (
     "qdc_circuit_new_devices",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
     "qdc_rq_plan", "qdc_spec_selftest", "qdc_gate_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
-    "qdc_jit_stats", "qdc_jit_dir", "qdc_spec_fingerprint",
+    "qdc_jit_stats", "qdc_jit_dir", "qdc_spec_fingerprint", "qdc_spec_selftest_batch",
 )
 
 
@@ -124,6 +124,10 @@ def _proto(lib):
                                            C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong), _S,
                                            C.c_char_p, _S]),
         "qdc_jit_stats": (_S, [C.POINTER(C.c_double), _S]),
+        "qdc_spec_selftest_batch": (C.c_char_p, [C.c_uint, C.POINTER(C.c_size_t), _S,
+                                                 C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                                                 C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong),
+                                                 C.c_char_p, _S]),
         "qdc_jit_dir": (_E, [C.c_char_p, _S]),
         "qdc_spec_fingerprint": (_E, [C.c_char_p, C.c_char_p, C.c_char_p,
                                       C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),

@@ -218,6 +218,12 @@ size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* kinds, co
 const char* qdc_spec_selftest(unsigned tile_bits, const unsigned* kinds, const unsigned* t1,
                               const unsigned* t2, const unsigned long long* deps, size_t n,
                               char* name_out, size_t cap);
+/* Test hook (host only): as qdc_spec_selftest for nprog pass programs at once (counts[p] stages
+ * each, the stage arrays concatenated), compiled in one call of the cache (as a circuit call
+ * compiles its missing kernels together).  names_out receives the kernel names, each NUL-ended. */
+const char* qdc_spec_selftest_batch(unsigned tile_bits, const size_t* counts, size_t nprog,
+                                    const unsigned* kinds, const unsigned* t1, const unsigned* t2,
+                                    const unsigned long long* deps, char* names_out, size_t cap);
 
 /* Test hook (host only): the launch geometry a single-gate op gets (qdc_device.hpp plan_gate)
  * on an n-qubit state: R = 2 (one-qubit, pos2 == pos1) or 4; two_states: the op reads both

@@ -294,21 +294,22 @@ def test_touched_headers_turn_specialization_off(tmp_path):
 
 
 def test_processes_of_a_job_compile_each_kernel_once(tmp_path):
-    """Four processes sharing one cache directory (the ranks of a multi-process job) ask for the
-    same kernels at the same moment: every kernel is compiled by exactly one of them (a
-    per-kernel lock), the others wait for it and use its code object."""
-    progs = _passes(10, 4)
+    """Four processes sharing one cache directory (the ranks of a multi-process job, two hipcc
+    processes each) ask for the same eight kernels at the same moment: every kernel is compiled
+    by exactly one of them (per-kernel locks, taken a compile batch at a time, so the processes
+    share the work), the others wait for it and use its code object."""
+    progs = _passes(10, 8)
     go = tmp_path / "go"
     code = f"""
         import os, time
         import quantum_differentiable_circuit as q
         while not os.path.exists({str(go)!r}):
             time.sleep(0.01)
-        names = [q.spec_selftest(11, st, dp)[0] for st, dp in {[(s, d) for s, d in progs]!r}]
+        names = q.spec_selftest_batch(11, {[(s, d) for s, d in progs]!r})
         s = q.jit_stats('f32')
         print(json.dumps([names, s['compiled'], s['waited']]))
         """
-    e = dict(os.environ, QDC_JIT_KEEP="0")
+    e = dict(os.environ, QDC_JIT_KEEP="0", QDC_JIT_JOBS="2")
     pre = (f"import sys, json; sys.path[:0] = [{str(ROOT)!r}, {str(PKG)!r}]\n")
     procs = [subprocess.Popen([sys.executable, "-c", pre + textwrap.dedent(code)], env=e,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -322,8 +323,9 @@ def test_processes_of_a_job_compile_each_kernel_once(tmp_path):
         assert p.returncode == 0, out + err
         res.append(json.loads(out.strip().splitlines()[-1]))
     names = {tuple(r[0]) for r in res}
-    assert len(names) == 1 and len(set(next(iter(names)))) == 4
-    assert sum(r[1] for r in res) == 4, res  # each kernel compiled once in the whole job
+    assert len(names) == 1 and len(set(next(iter(names)))) == 8
+    assert sum(r[1] for r in res) == 8, res  # each kernel compiled once in the whole job
+    assert sum(1 for r in res if r[1] > 0) >= 2, res  # by more than one process
     assert sum(r[2] for r in res) >= 1, res  # and someone waited for another's compile
 
 

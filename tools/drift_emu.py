@@ -123,7 +123,17 @@ def main():
     for a, p in reversed(fwd):
         x = apply(x, a.astype(DT).conj().T, p, DT)
     rows["fused fwd, rev = fwd^dagger"] = x
+    x = fused_fwd(x0)
+    for a, p in reversed(fwd):
+        x = apply(x, np.linalg.inv(a.astype(DT).astype(np.complex128)).astype(DT), p, DT)
+    rows["fused fwd, rev = inv(fwd) rounded"] = x
+    x = fused_fwd(x0)
+    for a, p in reversed(fwd):
+        x = apply(x, np.linalg.inv(a.astype(DT).astype(np.complex128)), p, DT, np.complex128)
+    rows["fused fwd, rev = inv(fwd) exact"] = x
     rows["fused, unrounded matrices"] = fused_rev(fused_fwd(x0, np.complex128), np.complex128)
+    rows["fused fwd rounded, rev unrounded"] = fused_rev(fused_fwd(x0), np.complex128)
+    rows["fused fwd unrounded, rev rounded"] = fused_rev(fused_fwd(x0, np.complex128))
     base = np.abs(rows["per-gate"] - ex).max()
     print(f"C5 n={n} {ng} gates: {len(fwd)} forward / {len(rev)} reverse stages "
           f"({len(order) / len(fwd):.2f} / {len(order) / len(rev):.2f} gates per stage)")
