@@ -263,6 +263,9 @@ struct Circuit {
   // one-state fused tile in chunks (QDC_TILE1_CHUNKS): TILE_CHUNKS_1, or TILE_CHUNKS_2 (f32: 2^11
   // amplitudes, one wave per tile on k_rw with five slots when QDC_RW bit 1 is set)
   uint32_t tile1_chunks = TILE_CHUNKS_1;
+  // runs of cotangent injections whose cotangents are all diagonal become one elementwise pass
+  // (k_diag_inject; QDC_DIAG_INJECT)
+  int diag_inject = 1;
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -327,6 +330,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
+    if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
     if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
       const uint32_t t = (uint32_t)atoi(e);
       if (t != TILE_CHUNKS_1 && t != TILE_CHUNKS_2)
@@ -1558,6 +1562,71 @@ struct Circuit {
     return nullptr;
   }
 
+  // --- diagonal cotangent injections ----------------------------------------------------------
+  // the injection's diagonal (G^T on its qubits has the diagonal of G), or false
+  bool diag_cotangent(const qdc_plan_op& op, const Flat& dg, const std::vector<size_t>& gidx) const {
+    if (op.type != QDC_PLAN_OP || !is_diff_density(ins[op.instr].kind)) return false;
+    const int R = is_q1_density(ins[op.instr].kind) ? 2 : 4;
+    if (op.pos2 >= (uint32_t)(4 * DI_GROUPS) || op.pos1 >= (uint32_t)(4 * DI_GROUPS)) return false;
+    if (R == 4 && op.pos2 / 4 != op.pos1 / 4) return false;  // both bits in one table group
+    const qdc_complex* g = dg.at(gidx[op.instr]);
+    for (int p = 0; p < R; ++p)
+      for (int q = 0; q < R; ++q)
+        if (p != q && (g[p * R + q].re != 0 || g[p * R + q].im != 0)) return false;
+    return true;
+  }
+  // Consecutive items that are injections only, all with diagonal cotangents, become one item of
+  // type 3 (their plan ops in order).  Injections only add to bwd from the (unchanged) fwd, so a
+  // run of them commutes and sums.
+  void merge_diag_injections(std::vector<Item>& items, const std::vector<qdc_plan_op>& pl,
+                             const Flat& dg, const std::vector<size_t>& gidx) const {
+    auto eligible = [&](const Item& it) {
+      if (it.type != 0 && it.type != 2) return false;
+      for (uint32_t k : it.ops)
+        if (!diag_cotangent(pl[k], dg, gidx)) return false;
+      return !it.ops.empty();
+    };
+    std::vector<Item> out;
+    for (Item& it : items) {
+      if (eligible(it)) {
+        if (!out.empty() && out.back().type == 3) {
+          out.back().ops.insert(out.back().ops.end(), it.ops.begin(), it.ops.end());
+          continue;
+        }
+        Item m;
+        m.type = 3;
+        m.ops = it.ops;
+        out.push_back(std::move(m));
+        continue;
+      }
+      out.push_back(std::move(it));
+    }
+    items = std::move(out);
+  }
+  // D(i) tables of a type-3 item: T[g * 16 + e] = sum of the diagonal entries that the densities
+  // on bits 4g..4g+3 select for the pattern e of those bits (summed in double); returns the
+  // number of groups in use
+  uint32_t diag_table(const Item& item, const std::vector<qdc_plan_op>& pl, const Flat& dg,
+                      const std::vector<size_t>& gidx, diag_tab& T) const {
+    cd acc[DI_GROUPS * 16] = {};
+    uint32_t ng = 1;
+    for (uint32_t k : item.ops) {
+      const qdc_plan_op& op = pl[k];
+      const bool q1 = is_q1_density(ins[op.instr].kind);
+      const int R = q1 ? 2 : 4;
+      const qdc_complex* gd = dg.at(gidx[op.instr]);
+      const uint32_t grp = op.pos2 / 4;
+      ng = std::max(ng, grp + 1);
+      for (uint32_t e = 0; e < 16; ++e) {
+        const uint32_t b2 = (e >> (op.pos2 % 4)) & 1u, b1 = (e >> (op.pos1 % 4)) & 1u;
+        const int r = q1 ? (int)b2 : (int)(2 * b2 + b1);
+        acc[grp * 16 + e] += cd(gd[r * R + r].re, gd[r * R + r].im);
+      }
+    }
+    for (int i = 0; i < DI_GROUPS * 16; ++i) T.t[i] = cx{(real)acc[i].real(), (real)acc[i].imag()};
+    return ng;
+  }
+
   // --- backward (Circuit::backward, circuit.rs:266-429) --------------------------------------
   const char* backward(const Flat& dg, const Flat& cg, const Flat& vg, qdc_complex* out) {
     std::vector<size_t> gidx;
@@ -1596,6 +1665,7 @@ struct Circuit {
         break;
       }
     std::vector<Item> items = fuse_items(pl, true, first_inject);
+    if (diag_inject) merge_diag_injections(items, pl, dg, gidx);
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
@@ -1604,6 +1674,16 @@ struct Circuit {
       fprintf(stderr, "backward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     for (const Item& item : items) {
+      if (item.type == 3) {  // a run of diagonal cotangent injections: one elementwise pass
+        diag_tab T;
+        const uint32_t ng = diag_table(item, pl, dg, gidx, T);
+        for (auto& s : sh) {
+          QDC_TRY(s.c().use());
+          QDC_TRY(qdc::diag_inject(s.c(), s.state, s.bwd, T, ng, nl, gm, have_bwd));
+        }
+        have_bwd = true;
+        continue;
+      }
       if (item.type == 2) {
         const bool two = item.ops[0] >= first_inject;
         if (two && !have_bwd) {  // the first injection is fused: it adds into a zero bwd

@@ -790,6 +790,21 @@ inline const char* pack(Ctx& c, const cx* src, cx* dst, const unsigned* victims,
                   reinterpret_cast<const chunk*>(src), reinterpret_cast<chunk*>(dst), pg);
 }
 
+// one run of diagonal cotangent injections (k_diag_inject): acc = false starts bwd
+inline const char* diag_inject(Ctx& c, const cx* f, cx* b, const diag_tab& T, uint32_t ngroups,
+                               uint32_t n, uint64_t gm, bool acc) {
+  const uint64_t amps = (uint64_t)1 << n;
+  const uint64_t nch = amps / VEC > 0 ? amps / VEC : 1;
+  if (amps < (uint64_t)VEC) return fail("internal: diagonal injection on a state below one chunk");
+  const uint32_t it = per_thread(nch, c.grid_cap);
+  const uint32_t grid = (uint32_t)((nch + (uint64_t)BLOCK * it - 1) / ((uint64_t)BLOCK * it));
+  const double bytes = (acc ? 3.0 : 2.0) * state_bytes(n);
+  const chunk* fc = reinterpret_cast<const chunk*>(f);
+  chunk* bc = reinterpret_cast<chunk*>(b);
+  if (acc) return c.launch("inject_diag", bytes, k_diag_inject<true>, grid, fc, bc, T, nch, it, gm, ngroups);
+  return c.launch("inject_diag", bytes, k_diag_inject<false>, grid, fc, bc, T, nch, it, gm, ngroups);
+}
+
 inline const char* set_standard(Ctx& c, cx* s, uint32_t n) {
   return elementwise<3>(c, nullptr, s, n);
 }

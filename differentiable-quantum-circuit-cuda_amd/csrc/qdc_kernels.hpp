@@ -1307,4 +1307,43 @@ __global__ __launch_bounds__(BLOCK) void k_elementwise(const cx* __restrict__ sr
   }
 }
 
+
+// Cotangent injections of a run of Diff densities whose (conjugated) cotangents are all
+// diagonal (a Z-basis observable: Re tr(rho Z) and its kin).  Each injects b += (G^T on its
+// qubits)(2 conj f) = 2 conj(f_i) G[k(i)][k(i)] with k(i) the density's bits of amplitude i, so
+// the whole run is one elementwise pass: b_i (+)= 2 conj(f_i) D(i), D(i) = sum_g T[g][bits 4g..4g+3
+// of i] (the host sums each density's diagonal into the table of the 4-bit group holding its
+// qubits).  ACC = false: the run starts the backward state (no read of b, no zeroing pass).
+constexpr int DI_GROUPS = 9;  // 4-bit groups of local amplitude bits 0..35
+struct diag_tab {
+  cx t[DI_GROUPS * 16];
+};
+template <bool ACC>
+__global__ __launch_bounds__(BLOCK) void k_diag_inject(const chunk* __restrict__ f,
+                                                       chunk* __restrict__ b, diag_tab T,
+                                                       uint64_t nch, uint32_t it, uint64_t gm,
+                                                       uint32_t ngroups) {
+  __shared__ cx lt[DI_GROUPS * 16];
+  for (uint32_t i = threadIdx.x; i < DI_GROUPS * 16; i += BLOCK) lt[i] = T.t[i];
+  __syncthreads();
+  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * it + threadIdx.x;
+  for (uint32_t step = 0; step < it; ++step) {
+    const uint64_t c = start + (uint64_t)step * BLOCK;
+    if (c >= nch) break;
+    const uint64_t di = c + (c & gm);
+    const chunk x = ldc(f + di);
+    chunk o;
+    if constexpr (ACC) o = ldc(b + di);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const uint64_t a = c * VEC + v;
+      cx d = lt[a & 15];
+      for (uint32_t g = 1; g < ngroups; ++g) d = cadd(d, lt[g * 16 + ((a >> (4 * g)) & 15)]);
+      // 2 conj(x) d
+      const cx y = {2 * (x.v[v].x * d.x + x.v[v].y * d.y), 2 * (x.v[v].x * d.y - x.v[v].y * d.x)};
+      o.v[v] = ACC ? cadd(o.v[v], y) : y;
+    }
+    stc(b + di, o);
+  }
+}
 }  // namespace qdc

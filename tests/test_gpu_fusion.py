@@ -428,3 +428,63 @@ print(json.dumps(q.jit_stats("f32")))
     grads = np.load(tmp_path / "prod_g.npy")
     fl.check("grads", grads, "ablation-then-production ")
     assert F.normrel(np.load(tmp_path / "abl_g.npy"), grads) > 1e-3, "the ablation build computed real gradients"
+
+
+def _diag_cots(seed):
+    """random complex diagonal cotangents (Q1 and Q2 densities): the diagonal-injection path"""
+    rng = np.random.default_rng(seed)
+
+    def cots(dens, dt):
+        return [np.ascontiguousarray(np.diag(rng.standard_normal(d.shape[0])
+                                             + 1j * rng.standard_normal(d.shape[0])).astype(dt))
+                for d in dens]
+    return cots
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("case", ["layered", "random", "sharded"])
+def test_diagonal_injections_equal_general(prec, case):
+    """Runs of cotangent injections whose cotangents are all diagonal (Z-basis observables) are one
+    elementwise pass (k_diag_inject: b (+)= 2 conj(f) D, D summed over the run's densities) instead
+    of the LDS injection passes; QDC_DIAG_INJECT=0 keeps the general path.  Both match the oracle's
+    floors and each other: densities at the end (layered: the run starts bwd), interleaved with
+    gates (random: Q1 and Q2 densities, runs accumulating into an existing bwd), and on 4 local
+    shards."""
+    import quantum_differentiable_circuit as q
+    n = 14 if case != "random" else 12
+    if case == "random":
+        ins, const, var = O.random_circuit(n, 160, seed=77, density_every=20)
+        psi0 = O.random_state(np.random.default_rng(5), n)
+    else:
+        ins, var = O.layered_circuit(n, 3, seed=61)
+        const, psi0 = [], None
+    fl = F.Floor(prec, n, ins, const, var, psi0=psi0, cots=_diag_cots(3), run=False)
+    kw = {"local_shards": 4} if case == "sharded" else {}
+    out = {}
+    for mode in ("0", "1"):
+        c = build_env(prec, n, ins, {"QDC_DIAG_INJECT": mode}) if not kw else None
+        if kw:
+            old = os.environ.get("QDC_DIAG_INJECT")
+            os.environ["QDC_DIAG_INJECT"] = mode
+            try:
+                c = q.circuit_class(prec)(n, **kw)
+            finally:
+                if old is None:
+                    del os.environ["QDC_DIAG_INJECT"]
+                else:
+                    os.environ["QDC_DIAG_INJECT"] = old
+            for kind, pos in ins:
+                c._push(kind, *pos)
+        if psi0 is not None:
+            c.set_state_from_vector(fl.psi0)
+        c.forward(fl.const, fl.var)
+        c.profile(True)
+        g = c.backward(fl.cots, fl.const, fl.var)
+        stats = c.profile_collect()
+        what = f"diag-inject {case} {prec} mode={mode} "
+        fl.check("grads", g, what)
+        if case != "sharded":
+            fl.check("bwd", c.get_state(2), what)
+        assert ("inject_diag" in stats) == (mode == "1"), sorted(stats)
+        out[mode] = g
+    F.check_pair(prec, out["1"], out["0"], fl.floor["grads"], f"diag-inject {case} {prec} on vs off grads")
