@@ -331,6 +331,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
+    if (const char* e = getenv("QDC_SCHED_CACHE")) sched_cache_on = atoi(e);
     if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
       const uint32_t t = (uint32_t)atoi(e);
       if (t != TILE_CHUNKS_1 && t != TILE_CHUNKS_2)
@@ -633,6 +634,7 @@ struct Circuit {
   }
 
   struct Item : FusionItem {
+    std::vector<std::vector<uint32_t>> stages;  // fused pass: its stages (stage_partition)
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t nstage = 0;  // fop count (stages) of the pass
     double flops_per_amp = 0;  // algorithmic real FLOPs per amplitude of the pass
@@ -666,9 +668,69 @@ struct Circuit {
     for (FusionItem& f : planner().fuse_items(plan, backward, first_inject)) {
       Item it;
       static_cast<FusionItem&>(it) = std::move(f);
+      if (it.type == 2) it.stages = stage_partition(it.ops, plan, backward);
       items.push_back(std::move(it));
     }
     return items;
+  }
+  // The pass schedule of a call (fuse_items + stage_partition, ~1-2 ms at C2 n = 28) depends on
+  // the plan, the inexact flags and the mode only, not on the gate values: the last schedule
+  // per direction is kept and reused when those are unchanged (QDC_SCHED_CACHE=0: off).
+  struct SchedCache {
+    bool valid = false;
+    size_t first_inject = 0;
+    std::vector<qdc_plan_op> in_plan, out_plan;
+    std::vector<uint8_t> inexact;
+    std::vector<Item> items;
+  };
+  SchedCache sched_cache[2];  // forward / run, backward
+  int sched_cache_on = 1;
+  static bool same_plan(const std::vector<qdc_plan_op>& a, const std::vector<qdc_plan_op>& b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); ++i) {
+      const qdc_plan_op &x = a[i], &y = b[i];
+      if (x.type != y.type || x.instr != y.instr || x.pos2 != y.pos2 || x.pos1 != y.pos1 ||
+          x.nvictims != y.nvictims || x.pack != y.pack)
+        return false;
+      for (unsigned k = 0; k < x.nvictims && k < 8; ++k)
+        if (x.victims[k] != y.victims[k]) return false;
+    }
+    return true;
+  }
+  std::vector<Item> schedule(std::vector<qdc_plan_op>& plan, bool backward, size_t first_inject) {
+    SchedCache& c = sched_cache[backward ? 1 : 0];
+    if (sched_cache_on && c.valid && c.first_inject == first_inject && c.inexact == inexact &&
+        same_plan(c.in_plan, plan)) {
+      plan = c.out_plan;
+      return c.items;
+    }
+    c.valid = false;
+    c.in_plan = plan;
+    std::vector<Item> items = fuse_items(plan, backward, first_inject);
+    if (sched_cache_on) {
+      c.out_plan = plan;
+      c.items = items;
+      c.inexact = inexact;
+      c.first_inject = first_inject;
+      c.valid = true;
+    }
+    return items;
+  }
+  // register-layout plans of passes (rq_plan, ~20 us each), by the pass's stages and tile
+  std::map<std::vector<uint64_t>, RqPlan> rq_plan_cache;
+  const RqPlan& rq_plan_cached(const std::vector<RqStage>& rs, uint32_t tbits, const uint32_t* src,
+                               bool maxcl, uint32_t ns) {
+    std::vector<uint64_t> key = {tbits, ns, maxcl ? 1u : 0u, src ? 1u : 0u};
+    if (src)
+      for (int i = 0; i < 4; ++i) key.push_back(src[i]);
+    for (const RqStage& r : rs) {
+      key.push_back(((uint64_t)r.kind << 48) | ((uint64_t)r.t1 << 24) | r.t2);
+      key.push_back(r.deps);
+    }
+    auto it = rq_plan_cache.find(key);
+    if (it != rq_plan_cache.end()) return it->second;
+    if (rq_plan_cache.size() >= 8192) rq_plan_cache.clear();
+    return rq_plan_cache.emplace(std::move(key), rq_plan(rs, tbits, src, maxcl, ns)).first->second;
   }
   std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
                                                      const std::vector<qdc_plan_op>& plan,
@@ -723,13 +785,9 @@ struct Circuit {
                             const std::vector<uint32_t>& out_idx, const Flat* dg) {
     stage_post.clear();
     if (spec_cache.size() >= 4096) spec_cache.clear();  // bounded; items of this call point into it
-    std::vector<std::vector<std::vector<uint32_t>>> stages_of(items.size());
     size_t nops = 0;
     for (size_t ii = 0; ii < items.size(); ++ii)
-      if (items[ii].type == 2) {
-        stages_of[ii] = stage_partition(items[ii].ops, plan, backward);
-        nops += stages_of[ii].size();
-      }
+      if (items[ii].type == 2) nops += items[ii].stages.size();
     if (nops == 0) return nullptr;
     // register-resident passes add relayout ops (<= one per stage, plus the return to L0) and
     // 12-cx layout descriptors (one per relayout, plus L0)
@@ -770,9 +828,9 @@ struct Circuit {
       std::vector<uint64_t> pq;  // their qubits (physical positions)
       std::vector<uint32_t> pc;  // their order classes (qdc_fusion.hpp)
       std::vector<int> pslot;    // their reduction slot (Gamma stages), else -1
-      pf.reserve(stages_of[ii].size());
+      pf.reserve(it.stages.size());
       const FusionPlanner PL = planner();
-      for (const auto& st : stages_of[ii]) {
+      for (const auto& st : it.stages) {
         uint64_t q = 0;
         uint32_t c = 0;
         for (uint32_t pi : st) {
@@ -788,7 +846,7 @@ struct Circuit {
           if (it.hb[r] == p - LV) return LV + it.lc + r;
         return 0xffffffffu;  // unreachable: tile_config covered every bit
       };
-      for (const auto& st : stages_of[ii]) {
+      for (const auto& st : it.stages) {
         if (is_meas(plan[st[0]])) {  // density (forward) or cotangent injection (backward)
           const qdc_plan_op& op = plan[st[0]];
           const Instr& in = ins[op.instr];
@@ -980,7 +1038,7 @@ struct Circuit {
                                    (rq_fwd5 && it.tbits == 12));  // k_rw W = 2, prefetching
       const uint32_t ns = (sizeof(real) == 4 && (s5_two || s5_one)) ? 5u : 4u;
       it.s5 = ns == 5;
-      const RqPlan P = rq_plan(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
+      const RqPlan& P = rq_plan_cached(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
       it.l0 = put_layout(P.load);
       {  // rqio after the load descriptor
         rqio io{};
@@ -1496,7 +1554,7 @@ struct Circuit {
     }
     mark_inexact(cg, vg, gidx);
     std::vector<qdc_plan_op> pl = plan(mode);
-    std::vector<Item> items = fuse_items(pl, false);
+    std::vector<Item> items = schedule(pl, false, SIZE_MAX);
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
@@ -1664,7 +1722,7 @@ struct Circuit {
         first_inject = i;
         break;
       }
-    std::vector<Item> items = fuse_items(pl, true, first_inject);
+    std::vector<Item> items = schedule(pl, true, first_inject);
     if (diag_inject) merge_diag_injections(items, pl, dg, gidx);
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
