@@ -11,6 +11,7 @@ result of the same f32 gate matrices.  Rows:
   fused fwd, rev = fwd^dagger   reverse aligned to the forward's rounded stage matrices
   fused, unrounded matrices     stage products applied in complex128, state rounded per stage
 usage: python3 tools/drift_emu.py [n] [gates]"""
+import os
 import sys
 from pathlib import Path
 
@@ -22,13 +23,16 @@ sys.path.insert(0, str(ROOT / "differentiable-quantum-circuit-cuda_amd"))
 import quantum_differentiable_circuit as q  # noqa: E402
 from quantum_differentiable_circuit import workloads as W  # noqa: E402
 
-DT = np.complex64
+DT = np.complex128 if os.environ.get("QDC_EMU_DT") == "c128" else np.complex64
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 14
     ng = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
-    ins, var = W.deep_random_circuit(n, ng, seed=33)
+    if len(sys.argv) > 3 and sys.argv[3] == "layered":  # C2's generator, ng layers
+        ins, var = W.layered_circuit(n, ng, 24)
+    else:
+        ins, var = W.deep_random_circuit(n, ng, seed=33)
     instr = [(k, *p) for k, p in ins]
     gm, vi = {}, 0
     for i, (k, p) in enumerate(ins):
@@ -59,14 +63,28 @@ def main():
         perm = [0, 2, 1, 3]
         return m[perm][:, perm]
 
-    def stages(mode, dag):
+    def stages(mode, dag, split_by=None):
+        """stage matrices of the schedule; split_by: gate -> forward stage id, and reverse stages
+        are cut where consecutive gates came from different forward stages (aligned stages)"""
         ops, items = q.fusion_schedule(n, instr, mode)
         out = []
         for it in items:
+            groups = []
             for st in it["stages"]:
                 gi = [ops[j]["instr"] for j in st if ops[j]["instr"] in gm]
                 if not gi:
                     continue
+                if split_by is None:
+                    groups.append(gi)
+                    continue
+                cur = [gi[0]]
+                for g in gi[1:]:
+                    if split_by[g] != split_by[cur[-1]]:
+                        groups.append(cur)
+                        cur = []
+                    cur.append(g)
+                groups.append(cur)
+            for gi in groups:
                 qs = sorted({b for i in gi for b in gm[i][1]})
                 lo, hi = qs[0], qs[-1]
                 a = np.eye(2 if lo == hi else 4, dtype=np.complex128)
@@ -74,7 +92,7 @@ def main():
                     k, p, g = gm[i]
                     m = full(k, g)
                     a = emb(k, p, m.conj().T if dag else m, lo, hi) @ a
-                out.append((a, (hi,) if lo == hi else (hi, lo)))
+                out.append((a, (hi,) if lo == hi else (hi, lo), gi))
         return out
 
     order = sorted(gm)
@@ -101,14 +119,16 @@ def main():
         return x
 
     fwd, rev = stages(1, False), stages(2, True)
+    fsid = {g: k for k, (_, _, gi) in enumerate(fwd) for g in gi}
+    rev_al = stages(2, True, fsid)
 
     def fused_fwd(x, mat_dt=None):
-        for a, p in fwd:
+        for a, p, _ in fwd:
             x = apply(x, a if mat_dt else a.astype(DT), p, DT, mat_dt)
         return x
 
-    def fused_rev(x, mat_dt=None):
-        for a, p in rev:
+    def fused_rev(x, mat_dt=None, st=None):
+        for a, p, _ in (rev if st is None else st):
             x = apply(x, a if mat_dt else a.astype(DT), p, DT, mat_dt)
         return x
 
@@ -120,15 +140,16 @@ def main():
         "per-gate fwd, fused rev": fused_rev(per_gate_fwd(x0)),
     }
     x = fused_fwd(x0)
-    for a, p in reversed(fwd):
+    for a, p, _ in reversed(fwd):
         x = apply(x, a.astype(DT).conj().T, p, DT)
     rows["fused fwd, rev = fwd^dagger"] = x
+    rows[f"fused, rev stages cut at fwd stages ({len(rev_al)})"] = fused_rev(fused_fwd(x0), st=rev_al)
     x = fused_fwd(x0)
-    for a, p in reversed(fwd):
+    for a, p, _ in reversed(fwd):
         x = apply(x, np.linalg.inv(a.astype(DT).astype(np.complex128)).astype(DT), p, DT)
     rows["fused fwd, rev = inv(fwd) rounded"] = x
     x = fused_fwd(x0)
-    for a, p in reversed(fwd):
+    for a, p, _ in reversed(fwd):
         x = apply(x, np.linalg.inv(a.astype(DT).astype(np.complex128)), p, DT, np.complex128)
     rows["fused fwd, rev = inv(fwd) exact"] = x
     rows["fused, unrounded matrices"] = fused_rev(fused_fwd(x0, np.complex128), np.complex128)
