@@ -266,6 +266,19 @@ struct Circuit {
   // runs of cotangent injections whose cotangents are all diagonal become one elementwise pass
   // (k_diag_inject; QDC_DIAG_INJECT)
   int diag_inject = 1;
+  // Mirrored schedules (QDC_MIRROR): the forward is scheduled on the two-state tile under both
+  // directions' rules (qdc_fusion.hpp FusionPlanner::mirror) and the backward runs its passes in
+  // reverse, uncomputing each stage with exactly the adjoint of the matrix the forward applied —
+  // the O(1)-memory uncompute then drifts like the reference's gate-by-gate U, U^dagger sequence
+  // instead of accumulating the rounding of independently formed stage products.  Unsharded
+  // circuits; the backward must follow a forward call with the same gates (else the backward
+  // schedules itself as usual).
+  int mirror = 0;
+  bool mirror_on() const {
+    return mirror && g == 0 && fuse && fuse_max_ops >= 2 && use_rq && (sizeof(real) == 4 || rq64);
+  }
+  // one-state one-wave five-slot passes on 2^11 tiles (f32): QDC_RW bit 1, or a mirrored forward
+  bool rw1() const { return (rq_wave & 2) || mirror_on(); }
 
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
@@ -331,6 +344,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
+    if (const char* e = getenv("QDC_MIRROR")) mirror = atoi(e);
     if (const char* e = getenv("QDC_SCHED_CACHE")) sched_cache_on = atoi(e);
     if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
       const uint32_t t = (uint32_t)atoi(e);
@@ -635,6 +649,8 @@ struct Circuit {
 
   struct Item : FusionItem {
     std::vector<std::vector<uint32_t>> stages;  // fused pass: its stages (stage_partition)
+    // a mirrored backward pass: per stage the forward (item, stage) it undoes
+    std::vector<std::pair<uint32_t, uint32_t>> mirror_of;
     size_t fop_off = 0;  // byte offset of the group's fop array in the pass program
     uint32_t nstage = 0;  // fop count (stages) of the pass
     double flops_per_amp = 0;  // algorithmic real FLOPs per amplitude of the pass
@@ -648,6 +664,76 @@ struct Circuit {
     // specialized kernel of a five-slot reverse pass or a one-state forward pass (qdc_jit.hpp): name, source, function
     SpecEntry* spec = nullptr;  // specialized kernel of the pass (qdc_jit.hpp), or none
   };
+  // what a mirrored backward needs from the forward call: its schedule (plan after the
+  // permuting passes' rewrites, items with stages), each gate stage's forward matrix (double,
+  // in the forward's frame) and the gates and inexact flags it was built from
+  struct MirrorRec {
+    bool valid = false;
+    std::vector<qdc_plan_op> plan;
+    std::vector<Item> items;
+    std::vector<std::vector<SMat>> stage_mats;  // [item][stage] (gate stages; else unused)
+    std::vector<qdc_complex> cgates, vgates;
+    std::vector<uint8_t> inexact;
+    std::vector<uint32_t> end_phys;  // the layout the forward left
+  } mrec;
+  std::vector<std::vector<SMat>>* rec_mats = nullptr;  // build_program records stage matrices here
+  // The backward schedule as the forward's passes run in reverse (mirror mode): op positions
+  // mapped into the layout each reverse pass starts from (the forward pass's store layout),
+  // stages and the ops in them reversed, the forward's swaps undone in reverse order.
+  bool mirror_schedule(std::vector<qdc_plan_op>& pl, std::vector<Item>& items,
+                       size_t& first_inject) const {
+    pl.clear();
+    items.clear();
+    const std::vector<Item>& F = mrec.items;
+    for (size_t k = F.size(); k-- > 0;) {
+      const Item& f = F[k];
+      if (f.type != 0 && f.type != 2) return false;  // remaps: unsharded circuits only
+      auto sigma = [&](uint32_t p) {
+        for (const auto& sw : f.swaps) {
+          if (p == sw.first) p = sw.second;
+          else if (p == sw.second) p = sw.first;
+        }
+        return p;
+      };
+      auto push = [&](uint32_t fi) {
+        qdc_plan_op op = mrec.plan[fi];
+        if (op.type == QDC_PLAN_OP) {
+          op.pos2 = sigma(op.pos2);
+          op.pos1 = sigma(op.pos1);
+        }
+        pl.push_back(op);
+        return (uint32_t)(pl.size() - 1);
+      };
+      Item b;
+      b.type = f.type;
+      b.lc = f.lc;
+      b.h = f.h;
+      for (uint32_t r = 0; r < (uint32_t)FMAX_ROWS; ++r) b.hb[r] = f.hb[r];
+      for (auto it = f.swaps.rbegin(); it != f.swaps.rend(); ++it) b.swaps.push_back(*it);
+      if (f.type == 2) {
+        for (size_t j = f.stages.size(); j-- > 0;) {
+          std::vector<uint32_t> st;
+          for (size_t t = f.stages[j].size(); t-- > 0;) {
+            const uint32_t bi = push(f.stages[j][t]);
+            st.push_back(bi);
+            b.ops.push_back(bi);
+          }
+          b.stages.push_back(std::move(st));
+          b.mirror_of.push_back({(uint32_t)k, (uint32_t)j});
+        }
+      } else {
+        b.ops.push_back(push(f.ops[0]));
+      }
+      items.push_back(std::move(b));
+    }
+    first_inject = pl.size();
+    for (size_t i = 0; i < pl.size(); ++i)
+      if (pl[i].type == QDC_PLAN_OP && is_diff_density(ins[pl[i].instr].kind)) {
+        first_inject = i;
+        break;
+      }
+    return true;
+  }
   static constexpr uint32_t TILE_CHUNKS_1 = FusionPlanner::TILE_CHUNKS_1;
   static constexpr uint32_t TILE_CHUNKS_2 = FusionPlanner::TILE_CHUNKS_2;
   FusionPlanner planner() const {
@@ -658,6 +744,7 @@ struct Circuit {
     P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
     P.tile1_chunks = tile1_chunks;
+    P.mirror = mirror_on();
     P.gamma_stage_cap = rq_gstage != 0;
     return P;
   }
@@ -846,7 +933,10 @@ struct Circuit {
           if (it.hb[r] == p - LV) return LV + it.lc + r;
         return 0xffffffffu;  // unreachable: tile_config covered every bit
       };
-      for (const auto& st : it.stages) {
+      if (rec_mats) (*rec_mats)[ii].clear();
+      for (size_t sj = 0; sj < it.stages.size(); ++sj) {
+        const auto& st = it.stages[sj];
+        if (rec_mats && is_meas(plan[st[0]])) (*rec_mats)[ii].push_back(smat_identity(2));
         if (is_meas(plan[st[0]])) {  // density (forward) or cotangent injection (backward)
           const qdc_plan_op& op = plan[st[0]];
           const Instr& in = ins[op.instr];
@@ -952,6 +1042,45 @@ struct Circuit {
           A = Anew;
           B = smat_mul(Eb, B);
         }
+        if (rec_mats) (*rec_mats)[ii].push_back(A);  // the forward's matrix, its own frame
+        // a mirrored backward stage uncomputes with exactly the adjoint of the forward's matrix
+        // (same rounding; the forward frame's two qubits may have swapped order under the
+        // forward pass's permutation)
+        SMat Aup = A;
+        if (backward && !it.mirror_of.empty()) {
+          bool nonu = false;
+          for (uint32_t pi : st) nonu = nonu || is_nonu(ins[plan[pi].instr].kind);
+          const auto& mo_ = it.mirror_of[sj];
+          if (!nonu && mo_.first < mrec.stage_mats.size() && mo_.second < mrec.stage_mats[mo_.first].size()) {
+            const SMat& Pf = mrec.stage_mats[mo_.first][mo_.second];
+            if (Pf.R == R) {
+              // forward lo / hi positions vs this stage's: swapped when the forward's lower
+              // qubit now sits above the other
+              uint32_t flo = 64, fhi = 0;
+              for (uint32_t fi : mrec.items[mo_.first].stages[mo_.second]) {
+                const qdc_plan_op& fo = mrec.plan[fi];
+                flo = std::min({flo, fo.pos2, fo.pos1});
+                fhi = std::max({fhi, fo.pos2, fo.pos1});
+              }
+              const auto& fsw = mrec.items[mo_.first].swaps;
+              auto sig = [&](uint32_t p) {
+                for (const auto& sw : fsw) {
+                  if (p == sw.first) p = sw.second;
+                  else if (p == sw.second) p = sw.first;
+                }
+                return p;
+              };
+              const bool swapped = R == 4 && sig(flo) > sig(fhi);
+              SMat At = Pf;
+              for (int pp = 0; pp < R; ++pp)
+                for (int qq = 0; qq < R; ++qq) {
+                  const int sp = swapped ? swap_bits4(pp) : pp, sq = swapped ? swap_bits4(qq) : qq;
+                  At.a[pp * R + qq] = std::conj(Pf.a[sq * R + sp]);
+                }
+              Aup = At;
+            }
+          }
+        }
         pf.emplace_back();
         pslot.push_back(-1);
         fop& F = pf.back();
@@ -963,7 +1092,7 @@ struct Circuit {
         it.writes_f = true;
         const int n = all_diag ? 4 : R * R;
         for (int i = 0; i < n; ++i) {
-          const cd va = all_diag ? A.a[i * 4 + i] : A.a[i];
+          const cd va = all_diag ? Aup.a[i * 4 + i] : Aup.a[i];
           const cd vb = all_diag ? B.a[i * 4 + i] : B.a[i];
           mats[mo + i] = cx{(real)va.real(), (real)va.imag()};
           mats[mo + n + i] = cx{(real)vb.real(), (real)vb.imag()};
@@ -1034,7 +1163,7 @@ struct Circuit {
       }
       // five register slots on the one-wave two-state f32 kernel (k_rw<.., S5>)
       const bool s5_two = two && rq5();
-      const bool s5_one = !two && ((rq_slots5 && (rq_wave & 2) && it.tbits == 11) ||  // k_rw W = 1
+      const bool s5_one = !two && ((rq_slots5 && rw1() && it.tbits == 11) ||  // k_rw W = 1
                                    (rq_fwd5 && it.tbits == 12));  // k_rw W = 2, prefetching
       const uint32_t ns = (sizeof(real) == 4 && (s5_two || s5_one)) ? 5u : 4u;
       it.s5 = ns == 5;
@@ -1060,7 +1189,7 @@ struct Circuit {
       const bool f32 = sizeof(real) == 4;
       const bool spec1 = spec_on() && spec_fwd && !two &&
                          (f32 ? ((!it.s5 && it.tbits == 12 && rq_prefetch && !(rq_wave & 2)) ||
-                                 (it.s5 && it.tbits == 11 && (rq_wave & 2)))
+                                 (it.s5 && it.tbits == 11 && rw1()))
                               : (it.tbits == 10 || it.tbits == 11));
       const bool spec = spec1 || (spec_on() && two && (f32 ? (it.s5 && rq5()) : it.tbits == 10));
       std::vector<SpecStep> sst;
@@ -1292,7 +1421,7 @@ struct Circuit {
       return ctx.launch_block(name, bytes, k_rw<false, 2, true, 1, true>, grid, 64u, f, b, fops,
                               mats, g, l0, partials, stride);
     }
-    if ((two ? (rq_wave & 1) : (rq_wave & 2)) && (nt == 128 || (nt == 256 && !two))) {
+    if ((two ? (rq_wave & 1) : rw1()) && (nt == 128 || (nt == 256 && !two))) {
       // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);
       const uint32_t bs = (!two && nt == 256) ? 128u : 64u;
@@ -1557,7 +1686,24 @@ struct Circuit {
     std::vector<Item> items = schedule(pl, false, SIZE_MAX);
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
-    QDC_TRY(build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr));
+    // a mirrored forward records what its backward will undo (forward mode only)
+    mrec.valid = false;
+    const bool record = mirror_on() && mode == QDC_MODE_FORWARD;
+    std::vector<std::vector<SMat>> mats_rec(record ? items.size() : 0);
+    rec_mats = record ? &mats_rec : nullptr;
+    const char* berr = build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr);
+    rec_mats = nullptr;
+    QDC_TRY(berr);
+    if (record) {
+      mrec.plan = pl;
+      mrec.items = items;
+      mrec.stage_mats = std::move(mats_rec);
+      const size_t nc = cg.size() ? cg.off.back() + cg.len.back() : 0;
+      const size_t nv = vg.size() ? vg.off.back() + vg.len.back() : 0;
+      mrec.cgates.assign(cg.data, cg.data + nc);
+      mrec.vgates.assign(vg.data, vg.data + nv);
+      mrec.inexact = inexact;
+    }
     if (rq_stats)
       fprintf(stderr, "forward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
@@ -1586,6 +1732,10 @@ struct Circuit {
       }
     }
     QDC_TRY(flush_all());
+    if (record) {  // (valid once every pass ran; the backward starts from this layout)
+      mrec.end_phys = layout.phys;
+      mrec.valid = true;
+    }
     std::vector<cx*> bufs;
     for (auto& s : sh) bufs.push_back(s.dens);
     QDC_TRY(ex.allreduce(sh, bufs, nout * RED));
@@ -1715,14 +1865,34 @@ struct Circuit {
     }
     bool have_bwd = false;
     mark_inexact(cg, vg, gidx);
-    std::vector<qdc_plan_op> pl = plan(QDC_PLAN_BACKWARD);
-    size_t first_inject = pl.size();
-    for (size_t i = 0; i < pl.size(); ++i)
-      if (pl[i].type == QDC_PLAN_OP && is_diff_density(ins[pl[i].instr].kind)) {
-        first_inject = i;
-        break;
-      }
-    std::vector<Item> items = schedule(pl, true, first_inject);
+    std::vector<qdc_plan_op> pl;
+    std::vector<Item> items;
+    size_t first_inject = 0;
+    // mirrored: the forward's passes in reverse, when this backward follows that forward with
+    // the same gates (else the backward schedules itself)
+    bool mirrored = false;
+    if (mirror_on() && mrec.valid && mrec.inexact == inexact && mrec.end_phys == layout.phys) {
+      const size_t nc = cg.size() ? cg.off.back() + cg.len.back() : 0;
+      const size_t nv = vg.size() ? vg.off.back() + vg.len.back() : 0;
+      const bool same = nc == mrec.cgates.size() && nv == mrec.vgates.size() &&
+                        (nc == 0 || std::memcmp(cg.data, mrec.cgates.data(), nc * sizeof(qdc_complex)) == 0) &&
+                        (nv == 0 || std::memcmp(vg.data, mrec.vgates.data(), nv * sizeof(qdc_complex)) == 0);
+      mirrored = same && mirror_schedule(pl, items, first_inject);
+    }
+    mrec.valid = false;  // (this backward changes the layout and the state)
+    if (!mirrored) {
+      pl = plan(QDC_PLAN_BACKWARD);
+      first_inject = pl.size();
+      for (size_t i = 0; i < pl.size(); ++i)
+        if (pl[i].type == QDC_PLAN_OP && is_diff_density(ins[pl[i].instr].kind)) {
+          first_inject = i;
+          break;
+        }
+      // QDC_MIRROR=2 (tests): a backward that cannot mirror its forward is an error
+      if (mirror_on() && mirror == 2)
+        return fail("mirror: the backward does not follow a forward call with the same gates");
+      items = schedule(pl, true, first_inject);
+    }
     if (diag_inject) merge_diag_injections(items, pl, dg, gidx);
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();

@@ -87,6 +87,12 @@ struct FusionPlanner {
   // low physical positions a permuting pass fills with the qubits the next ops need first
   // (>= NLOW; more makes the next tiles' contiguous runs longer)
   uint32_t perm_low = (uint32_t)LV + 3;
+  // Mirrored schedules: the forward is scheduled so that its passes, run in reverse, are the
+  // backward's passes (qdc_circuit.hpp mirror_backward): on the two-state tile, under the
+  // ordering rules of both directions, passes of densities only or of gates only, and the
+  // backward's cap on Gamma stages (stages holding a variable gate).  The uncompute then applies
+  // exactly the adjoints of the forward's stage matrices.
+  bool mirror = false;
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -147,6 +153,9 @@ struct FusionPlanner {
   uint32_t op_class(const qdc_plan_op& op, bool backward) const {
     if (op.type != QDC_PLAN_OP) return 0;
     const bool inex = op.instr < inexact.size() && inexact[op.instr];
+    // a mirrored forward keeps the backward's order relations too
+    if (mirror && !backward)
+      return order_class(ins[op.instr].kind, false, inex) | order_class(ins[op.instr].kind, true, inex);
     return order_class(ins[op.instr].kind, backward, inex);
   }
   static uint32_t conflicts_of(uint32_t c) { return order_conflicts(c); }
@@ -216,8 +225,20 @@ struct FusionPlanner {
   std::vector<FusionItem> fuse_items(std::vector<qdc_plan_op>& plan, bool backward,
                                      size_t first_inject = SIZE_MAX) const {
     std::vector<FusionItem> items;
-    const uint32_t T = log2_of(backward ? tile2_chunks : tile1_chunks);
+    const bool mfwd = mirror && !backward;  // a mirrored forward (see `mirror`)
+    const uint32_t T = log2_of((backward || mfwd) ? tile2_chunks : tile1_chunks);
     const bool on = fuse && fuse_max_ops >= 2;
+    // a mirrored forward's passes do not straddle the last differentiable density: the
+    // backward's passes before its first injection are one-state (no cotangent yet)
+    size_t msplit = SIZE_MAX;
+    if (mfwd)
+      for (size_t k = plan.size(); k-- > 0;)
+        if (plan[k].type == QDC_PLAN_OP && is_meas(plan[k]) &&
+            (ins[plan[k].instr].kind == QDC_DIFF_Q1_DENSITY ||
+             ins[plan[k].instr].kind == QDC_DIFF_Q2_DENSITY)) {
+          msplit = k + 1;
+          break;
+        }
     auto fusable = [&](size_t k) {
       const qdc_plan_op& op = plan[k];
       if (!(is_gate_op(op) || (fuse_meas && is_meas(op))) || !tile_fits(op_bits(op), T))
@@ -240,9 +261,10 @@ struct FusionPlanner {
       }
       size_t j = i;
       while (j < plan.size() && plan[j].type == QDC_PLAN_OP && fusable(j) &&
-             !(backward && j == first_inject && j > i))
+             !(backward && j == first_inject && j > i) && !(j == msplit && j > i))
         ++j;
-      const bool two = backward && i >= first_inject;
+      // (a mirrored forward's passes are capped as the backward's two-state passes)
+      const bool two = (backward && i >= first_inject) || mfwd;
       const bool gstage = two && rq_grad && gamma_stage_cap;
       const uint32_t gmax = gstage ? fuse_max_ops
                             : (two && rq_grad) ? (uint32_t)FMAX_GRAD_RQ : (uint32_t)FMAX_GRAD;
@@ -259,9 +281,10 @@ struct FusionPlanner {
           const uint64_t q = (1ull << g.pos2) | (1ull << g.pos1);
           const bool meas = is_meas(g);
           const uint32_t cls = op_class(g, backward);
-          const uint32_t isred =
-              ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
-          if ((backward && kind >= 0 && (int)meas != kind) || (q & blocked) ||
+          const uint32_t isred = mfwd ? ((meas || is_var(ins[g.instr].kind)) ? 1u : 0u)
+                                 : ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
+          if (((backward || mfwd) && kind >= 0 && (int)meas != kind) || (q & blocked) ||
+              (mfwd && meas && nred + 1 > (uint32_t)FMAX_GRAD) ||
               (conflicts_of(cls) & left) || pass.size() >= fuse_max_ops ||
               nred + isred > gmax || !tile_fits(mask | op_bits(g), T)) {
             blocked |= q;
@@ -278,7 +301,7 @@ struct FusionPlanner {
         // depends on a dropped one) until its Gamma stages fit the accumulators
         if (gstage && nred > (uint32_t)FMAX_GRAD_RQ) {
           bool cut = false;
-          while (pass.size() > 1 && gamma_stages(pass, plan) > (uint32_t)FMAX_GRAD_RQ) {
+          while (pass.size() > 1 && gamma_stages(pass, plan, !mfwd) > (uint32_t)FMAX_GRAD_RQ) {
             rest.push_back(pass.back());
             pass.pop_back();
             cut = true;
@@ -306,10 +329,10 @@ struct FusionPlanner {
     return items;
   }
 
-  uint32_t gamma_stages(const std::vector<uint32_t>& pass,
-                        const std::vector<qdc_plan_op>& plan) const {
+  uint32_t gamma_stages(const std::vector<uint32_t>& pass, const std::vector<qdc_plan_op>& plan,
+                        bool backward = true) const {
     uint32_t n = 0;
-    for (const auto& st : stage_partition(pass, plan, true)) {
+    for (const auto& st : stage_partition(pass, plan, backward)) {
       bool var = false;
       for (uint32_t k : st) var = var || (plan[k].type == QDC_PLAN_OP && is_var(ins[plan[k].instr].kind));
       n += var ? 1u : 0u;

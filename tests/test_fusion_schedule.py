@@ -68,7 +68,7 @@ def qubits(ins, op):
     return set(p)
 
 
-def check_invariants(n, ins, sens, mode, prec, ops, items, permuted=False):
+def check_invariants(n, ins, sens, mode, prec, ops, items, permuted=False, tbits=None):
     backward = mode == 2
     order = [i for it in items for st in it["stages"] for i in st]
     assert sorted(order) == list(range(len(ops)))
@@ -92,7 +92,7 @@ def check_invariants(n, ins, sens, mode, prec, ops, items, permuted=False):
             if share or clash:
                 assert pos[a] < pos[b], (a, b, ops[a], ops[b])
     first_inject = next((i for i, m in enumerate(meas) if m), len(ops)) if backward else len(ops)
-    tbits = T[2 if backward else 1]
+    tbits = tbits or T[2 if backward else 1]
     for it in items:
         if it["type"] != 2:
             assert len(it["stages"]) == 1 and len(it["stages"][0]) == 1
@@ -217,6 +217,76 @@ def test_schedule_replay_matches_sequential_oracle(monkeypatch, perturb, sched_r
     want_g = o.backward(cot_fn(want_d), const, var)
     got_d, got_g, final = replay(n, ins, ops, items, gates, psi0, cot_fn)
     assert len(got_d) == len(want_d) and len(got_g) == len(want_g)
+    for a, b in zip(got_d, want_d):
+        assert np.abs(a - b).max() < 1e-12
+    ga, gb = np.concatenate(got_g), np.concatenate(want_g)
+    assert np.abs(ga - gb).max() < 1e-11 * np.abs(gb).max()
+    assert np.abs(final - o.state).max() < 1e-11
+
+
+def mirrored(ops_f, items_f):
+    """The backward schedule QDC_MIRROR runs (qdc_circuit.hpp mirror_schedule): the forward's
+    passes in reverse, stages and the ops in them reversed.  Forward plan index i is backward
+    plan index L - 1 - i (both plans hold the gates and differentiable densities)."""
+    L = len(ops_f)
+    items = []
+    for it in reversed(items_f):
+        st = [[L - 1 - i for i in reversed(s)] for s in reversed(it["stages"])]
+        items.append(dict(it, stages=st))
+    return ops_f[::-1], items
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("sched_rq", ["0", "1"])
+@pytest.mark.parametrize("n,seed,perturb", [(14, 1, 0.0), (17, 2, 1e-3), (24, 3, 0.0)])
+def test_mirrored_schedule_invariants(monkeypatch, prec, sched_rq, n, seed, perturb):
+    """QDC_MIRROR: the forward is scheduled on the two-state tile so that its passes run in
+    reverse are a valid reverse sweep - the invariants of both directions hold, passes are
+    densities only or gates only, none spans the last differentiable density, and the Gamma
+    stages (stages holding a variable gate) of a pass fit the 16 accumulators."""
+    monkeypatch.setenv("QDC_SCHED_RQ", sched_rq)
+    monkeypatch.setenv("QDC_SCHED_MIRROR", "1")
+    ins, const, var, gates, sens = make(n, seed, perturb)
+    ops_f, items_f = schedule(n, ins, 1, sens, prec)
+    perm = sched_rq == "1"
+    check_invariants(n, ins, sens, 1, prec, ops_f, items_f, permuted=perm, tbits=T[2])
+    ops_b, items_b = mirrored(ops_f, items_f)
+    check_invariants(n, ins, sens, 2, prec, ops_b, items_b, permuted=perm, tbits=T[2])
+    var_kinds = set(Q1 + Q2 + DIAG) - set(CONST)
+    for it in items_f:
+        if it["type"] != 2:
+            continue
+        members = [i for st in it["stages"] for i in st]
+        assert len({ins[ops_f[i]["instr"]][0] in DENS for i in members}) == 1
+        gst = sum(any(ins[ops_f[i]["instr"]][0] in var_kinds for i in st) for st in it["stages"])
+        assert gst <= 16
+    assert sum(it["type"] == 2 for it in items_f) > 3
+
+
+@pytest.mark.parametrize("sched_rq", ["0", "1"])
+def test_mirrored_schedule_replay_matches_sequential_oracle(monkeypatch, sched_rq):
+    """The mirrored reverse sweep, replayed with the oracle's primitives, gives the sequential
+    densities and gradients (non-unitary matrices on unitary kinds included)."""
+    monkeypatch.setenv("QDC_SCHED_RQ", sched_rq)
+    monkeypatch.setenv("QDC_SCHED_MIRROR", "1")
+    n = 12
+    ins, const, var, gates, sens = make(n, 11, 1e-3)
+    ops, items = {}, {}
+    ops["fwd"], items["fwd"] = schedule(n, ins, 1, sens, "f32")
+    ops["bwd"], items["bwd"] = mirrored(ops["fwd"], items["fwd"])
+    assert sum(it["type"] == 2 for it in items["fwd"]) > 3
+    psi0 = O.random_state(np.random.default_rng(5), n)
+    o = O.OracleCircuit(n)
+    for k, p in ins:
+        o.add(k, *p)
+    o.set_state_from_vector(psi0)
+    want_d = o.forward(const, var)
+
+    def cot_fn(d):
+        return [c.conj() for c in O.tsallis_loss_and_cotangents(d)[1]]
+
+    want_g = o.backward(cot_fn(want_d), const, var)
+    got_d, got_g, final = replay(n, ins, ops, items, gates, psi0, cot_fn)
     for a, b in zip(got_d, want_d):
         assert np.abs(a - b).max() < 1e-12
     ga, gb = np.concatenate(got_g), np.concatenate(want_g)
