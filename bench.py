@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # vector peak (MI355X_MICROARCH.md; packed f32)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -61,7 +61,7 @@ def parse():
                     help="time one whole C3 call on the CPU when its projection is below this")
     ap.add_argument("--pmc", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--micro", action="store_true", help="per-kernel bandwidth sweep")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None, devices=None):
@@ -435,7 +435,7 @@ def abi_unfused_sample(args, n):
                     "host sync per gradient, a new state per density injection)"}
 
 
-def micro(args, n=None, verbose=True):
+def micro(args, n=None, verbose=True, q1_positions=None, q2_pairs=None):
     """Per-kernel bandwidth: each gate kind at every position, forward and fused reverse
     (single-gate kernels: fusion off).  Returns (case, kernel, launches, median ms, GB/s) rows."""
     import quantum_differentiable_circuit as q
@@ -482,14 +482,15 @@ def micro(args, n=None, verbose=True):
         del c
 
     reps = 8
-    for pos in range(n):
+    for pos in (range(n) if q1_positions is None else q1_positions):
         def s1(c, pos=pos):
             for _ in range(reps):
                 c.add_q1_var_gate(pos)
             c.get_q1_dens_op_with_grad(pos)
             return [np.ascontiguousarray(O_haar(rng, 2), dtype=dt) for _ in range(reps)]
         run(f"q1 {pos}", s1)
-    for pos2, pos1 in [(0, 1), (1, 0), (5, 20), (26, 27), (27, 0), (1, 2), (3, 9), (14, 13)]:
+    pairs = [(0, 1), (1, 0), (5, 20), (26, 27), (27, 0), (1, 2), (3, 9), (14, 13)]
+    for pos2, pos1 in (pairs if q2_pairs is None else q2_pairs):
         if max(pos2, pos1) >= n:
             continue
 

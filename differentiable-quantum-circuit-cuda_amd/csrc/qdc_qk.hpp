@@ -60,8 +60,10 @@ inline void qk_operands(const cx* U, std::vector<real>& a) {
 // P = 2 (f32, qubit 0 not a target): lane j of quad q owns the adjacent groups 2j and 2j + 1,
 // whose amplitudes at each offset form one 16-B chunk — every load and store is 16 B per lane
 // (256 contiguous bytes per quad) and each batch runs the MFMA chain twice.  P = 1: one group
-// per lane, 8-B (f32) accesses.
-template <int K, int P, int NB>
+// per lane, 8-B (f32) accesses.  PF: the next iteration's batches are loaded before this one's
+// MFMA chains run (software pipelining: HBM latency hidden behind the matrix cores in every
+// wave, not only across waves).
+template <int K, int P, int NB, bool PF = false>
 __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __restrict__ aop,
                                             qk_geo g) {
   constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
@@ -86,29 +88,33 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
   const uint64_t nbatch = (g.ngroups + GB - 1) / GB;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t bt0 = wave * NB; bt0 < nbatch; bt0 += nwaves * NB) {
+  struct batch {
     uint64_t base[NB];
     bool live[NB];
     cx x[NB][P][M];
+  };
+  auto load = [&](uint64_t bt0, batch& B) __attribute__((always_inline)) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const uint64_t grp = (bt0 + nb) * GB + (uint64_t)j * P;
-      live[nb] = grp < g.ngroups;  // ngroups is even when P = 2 (k < n)
-      base[nb] = grp;
+      B.live[nb] = grp < g.ngroups;  // ngroups is even when P = 2 (k < n)
+      B.base[nb] = grp;
 #pragma unroll
-      for (int b = 0; b < K; ++b) base[nb] = insert_zero(base[nb], g.sorted[b]);
+      for (int b = 0; b < K; ++b) B.base[nb] = insert_zero(B.base[nb], g.sorted[b]);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         if constexpr (P == 2) {
-          const chunk c = live[nb] ? ldc(reinterpret_cast<const chunk*>(s + base[nb] + off[m]))
-                                   : chunk{};
-          x[nb][0][m] = c.v[0];
-          x[nb][1][m] = c.v[1];
+          const chunk c = B.live[nb] ? ldc(reinterpret_cast<const chunk*>(s + B.base[nb] + off[m]))
+                                     : chunk{};
+          B.x[nb][0][m] = c.v[0];
+          B.x[nb][1][m] = c.v[1];
         } else {
-          x[nb][0][m] = live[nb] ? s[base[nb] + off[m]] : cx{0, 0};
+          B.x[nb][0][m] = B.live[nb] ? s[B.base[nb] + off[m]] : cx{0, 0};
         }
       }
     }
+  };
+  auto apply_store = [&](const batch& B) __attribute__((always_inline)) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
@@ -119,7 +125,7 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
           d[p] = acc_t{0, 0, 0, 0};
 #pragma unroll
           for (int u = 0; u < S; ++u) {
-            const real bv = (u & 1) ? x[nb][p][u >> 1].y : x[nb][p][u >> 1].x;
+            const real bv = (u & 1) ? B.x[nb][p][u >> 1].y : B.x[nb][p][u >> 1].x;
 #ifdef QDC_F64
             d[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][u], bv, d[p], 0, 0, 0);
 #else
@@ -127,21 +133,43 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
 #endif
           }
         }
-        if (live[nb]) {
+        if (B.live[nb]) {
           if constexpr (P == 2) {
             chunk c0, c1;
             c0.v[0] = cx{d[0][0], d[0][1]};
             c0.v[1] = cx{d[1][0], d[1][1]};
             c1.v[0] = cx{d[0][2], d[0][3]};
             c1.v[1] = cx{d[1][2], d[1][3]};
-            stc(reinterpret_cast<chunk*>(s + base[nb] + off[2 * t]), c0);
-            stc(reinterpret_cast<chunk*>(s + base[nb] + off[2 * t + 1]), c1);
+            stc(reinterpret_cast<chunk*>(s + B.base[nb] + off[2 * t]), c0);
+            stc(reinterpret_cast<chunk*>(s + B.base[nb] + off[2 * t + 1]), c1);
           } else {
-            s[base[nb] + off[2 * t]] = cx{d[0][0], d[0][1]};
-            s[base[nb] + off[2 * t + 1]] = cx{d[0][2], d[0][3]};
+            s[B.base[nb] + off[2 * t]] = cx{d[0][0], d[0][1]};
+            s[B.base[nb] + off[2 * t + 1]] = cx{d[0][2], d[0][3]};
           }
         }
       }
+    }
+  };
+  const uint64_t step = nwaves * NB;
+  if constexpr (!PF) {
+    for (uint64_t bt0 = wave * NB; bt0 < nbatch; bt0 += step) {
+      batch B;
+      load(bt0, B);
+      apply_store(B);
+    }
+  } else {
+    // two register sets, the loop unrolled by two so neither is copied
+    batch B0, B1;
+    uint64_t bt0 = wave * NB;
+    if (bt0 < nbatch) load(bt0, B0);
+    while (bt0 < nbatch) {
+      if (bt0 + step < nbatch) load(bt0 + step, B1);
+      apply_store(B0);
+      bt0 += step;
+      if (bt0 >= nbatch) break;
+      if (bt0 + step < nbatch) load(bt0 + step, B0);
+      apply_store(B1);
+      bt0 += step;
     }
   }
 }
@@ -219,7 +247,12 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   // bytes in flight per wave) at k >= 4 — measured at n = 28 (tools/qk_probe.py,
   // profiles/r2o_qk_probe.log): k = 3 neutral, k = 4 +2 %, k = 5 +7 %.  Knob QDC_QK_WIDE=0/1
   const char* ew = getenv("QDC_QK_WIDE");
-  const bool wide = ew ? atoi(ew) != 0 : k >= 4;
+  bool wide = ew ? atoi(ew) != 0 : k >= 4;
+  // software-pipelined batches (k_qk PF; knob QDC_QK_PF=0/1): NB batches in flight while the
+  // previous NB run on the matrix cores — replaces "wide" (same registers)
+  const char* epf = getenv("QDC_QK_PF");
+  const bool pf = epf ? atoi(epf) != 0 : false;
+  if (pf) wide = false;
   const uint64_t nb = (k == 3 ? 4 : k == 4 ? 2 : 1) * (wide ? 2 : 1);
   const uint64_t gpb = pair ? 32 : 16;  // groups per batch
   const uint64_t waves = ((g.ngroups + gpb - 1) / gpb + nb - 1) / nb;
@@ -229,8 +262,9 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   const real* buf = ring.dev[slot];
   const char* e;
 #define QDC_QK_LAUNCH(KK, PP, NB3)                                                              \
-  e = wide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3)>, grid, 256u, s, buf, g)     \
-           : c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3)>, grid, 256u, s, buf, g)
+  e = pf     ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3), true>, grid, 256u, s, buf, g) \
+      : wide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3)>, grid, 256u, s, buf, g)   \
+             : c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3)>, grid, 256u, s, buf, g)
 #ifndef QDC_F64
   if (pair) {
     if (k == 3) QDC_QK_LAUNCH(3, 2, 4);
