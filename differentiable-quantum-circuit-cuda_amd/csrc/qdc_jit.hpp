@@ -190,7 +190,7 @@ inline std::string spec_kernel_source(const std::string& name, const std::string
   const std::string args =
       K.two ? "qdc::cx (&xf)[" + R + "], qdc::cx (&xb)[" + R + "], const qdc::SpecEnv& E"
             : "qdc::cx (&x)[" + R + "], const qdc::SpecEnv& E";
-  return "#include \"qdc_spec.hpp\"\n"
+  return "#define QDC_SPEC_TU 1\n#include \"qdc_spec.hpp\"\n"
          "namespace {\n"
          "struct Prog {\n"
          "  __device__ __forceinline__ void operator()(" + args + ") const {\n"

@@ -556,6 +556,7 @@ struct fin_table {
 
 // Granule partials of a dynamic-tail pass, pre-summed: block (slot y, chunk x) adds the BLOCK
 // partials x*BLOCK .. of slot y by a fixed tree (block_reduce_store) into one chunk partial.
+#ifndef QDC_SPEC_TU  // (not in the specialized kernels' translation units)
 __global__ __launch_bounds__(BLOCK) void k_dsum(const cx* __restrict__ parts, uint64_t stride,
                                                 uint32_t n, cx* __restrict__ out,
                                                 uint64_t out_stride) {
@@ -566,9 +567,11 @@ __global__ __launch_bounds__(BLOCK) void k_dsum(const cx* __restrict__ parts, ui
   for (int k = 0; k < RED; ++k) acc[k] = g < n ? p[k] : cx{0, 0};
   block_reduce_store<RED>(acc, out + (uint64_t)blockIdx.y * out_stride + (uint64_t)blockIdx.x * RED);
 }
+#endif  // QDC_SPEC_TU
 
 // one slot per block: the sum of its nblocks block partials, then of its n2 granule partials
 // (dynamic-tail passes, fgeo::dpart) — a fixed order, so the result is deterministic
+#ifndef QDC_SPEC_TU  // (not in the specialized kernels' translation units)
 __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ partials,
                                                     uint64_t slot_stride, uint32_t nblocks,
                                                     fin_table tab, cx* __restrict__ dst,
@@ -592,6 +595,7 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
     *d = accumulate ? cadd(*d, out[threadIdx.x]) : out[threadIdx.x];
   }
 }
+#endif  // QDC_SPEC_TU
 
 
 // ---------------------------------------------------------------------------------------
@@ -1251,6 +1255,7 @@ struct packgeo {
   uint32_t vc[8];  // victim chunk bits, ascending
 };
 
+#ifndef QDC_SPEC_TU  // (not in the specialized kernels' translation units)
 __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
                                                 chunk* __restrict__ dst, packgeo pg) {
   const uint64_t o = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -1261,6 +1266,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
   for (uint32_t k = 0; k < pg.g; ++k) idx |= ((j >> k) & 1ull) << pg.vc[k];
   stc(dst + o, ldc(src + idx));
 }
+#endif  // QDC_SPEC_TU
 
 // ---------------------------------------------------------------------------------------
 // Elementwise state kernels (primitives.cu:176-187, 879-939).
