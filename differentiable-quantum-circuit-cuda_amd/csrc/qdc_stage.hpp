@@ -14,7 +14,10 @@
 //   (get_q{1,2}_grad, circuit.rs:320-392; primitives.cu:202-354).
 //
 // Stage basis: index r = 2*bit(hi) + bit(lo) (a one-qubit stage: r = bit).  Products are
-// formed in double on the host; the device gets them rounded to the state precision.
+// formed on the host in a wider type than the state's (f32 states: double; f64 states: x87
+// long double, 64-bit significand) and rounded once to the state precision for the device: a
+// stage matrix then differs from the exact product of its gates by half an ulp of the state
+// precision, as a single gate's matrix does, instead of by the rounding of every product step.
 #pragma once
 
 #include <complex>
@@ -22,7 +25,12 @@
 
 namespace qdc {
 
-using cd = std::complex<double>;
+#ifdef QDC_F64
+using hreal = long double;
+#else
+using hreal = double;
+#endif
+using cd = std::complex<hreal>;
 
 struct SMat {  // R x R, row-major, R = 2 or 4
   int R = 4;
@@ -42,9 +50,13 @@ inline SMat smat_mul(const SMat& x, const SMat& y) {
   const int R = x.R;
   for (int p = 0; p < R; ++p)
     for (int q = 0; q < R; ++q) {
-      cd s = 0;
-      for (int k = 0; k < R; ++k) s += x.a[p * R + k] * y.a[k * R + q];
-      z.a[p * R + q] = s;
+      hreal sr = 0, si = 0;  // (real arithmetic: no complex-multiply NaN/Inf recovery path)
+      for (int k = 0; k < R; ++k) {
+        const cd u = x.a[p * R + k], v = y.a[k * R + q];
+        sr += u.real() * v.real() - u.imag() * v.imag();
+        si += u.real() * v.imag() + u.imag() * v.real();
+      }
+      z.a[p * R + q] = cd(sr, si);
     }
   return z;
 }
