@@ -549,6 +549,7 @@ def main():
     warmup_s = time.perf_counter() - tw  # includes the specialized kernels' compilation
 
     c.profile(True)
+    c.host_times(reset=True)
     barrier(comm)
     c.synchronize()
     t0 = time.perf_counter()
@@ -560,6 +561,11 @@ def main():
     barrier(comm)
     stats = c.profile_collect()
     c.profile(False)
+    # host milliseconds per step by phase (rank 0): scheduling and program building sit before a
+    # call's first launch, so they are device idle time unless the previous call still runs
+    ht = c.host_times()
+    host_ms = {d: {k: round(v / args.steps, 3) for k, v in ht[d].items() if k != "calls"}
+               for d in ht}
 
     # per rank: the specialized-kernel cache (compile / wait seconds, kernels compiled by this
     # rank: one rank compiles each kernel of a job) and the all-to-all time per step, so a first
@@ -693,6 +699,7 @@ def main():
                          "algo_flops_per_launch": dom_flops}
                         if dom_flops > 0 else None),
             "kernels": kernels,
+            "host_ms_per_step": host_ms,
             "ranks": per_rank,
             "effective_gate_bandwidth": effective,
             "micro_min": (gate_kernels or {}).get("micro_min") if isinstance(gate_kernels, dict) else None,

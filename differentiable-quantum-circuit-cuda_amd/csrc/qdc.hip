@@ -417,6 +417,20 @@ QDC_API size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out,
   return qdc::prof_collect(xs, out, cap);
 }
 
+// Host time of the circuit's calls since the last reset: out[0..5] run/forward, out[6..11]
+// backward, each (calls, setup ms, schedule ms, program-build ms, launch ms, finish ms: stream
+// sync, result copies and gradient reconstruction).  Returns the values written.
+QDC_API size_t qdc_circuit_host_times(qdc_circuit* c, double* out, size_t n, int reset) {
+  size_t k = 0;
+  for (int d = 0; d < 2; ++d)
+    for (int j = 0; j < 6; ++j, ++k)
+      if (out && k < n) out[k] = c->impl.host_ms[d][j];
+  if (reset)
+    for (auto& row : c->impl.host_ms)
+      for (double& v : row) v = 0;
+  return std::min<size_t>(n, 12);
+}
+
 QDC_API const char* qdc_build_info(void) {
 #ifdef QDC_F64
   return "qdc f64 gfx950";

@@ -229,6 +229,18 @@ struct Circuit {
   int fuse_meas = 1;        // densities / cotangent injections join fused passes
   int use_rq = 1;           // f32 gate passes run register-resident (qdc_rq.hpp)
   int rq_stats = 0;
+  // host time of the calls (qdc_circuit_host_times): per direction (0 run/forward, 1 backward)
+  // the calls and the milliseconds of setup, scheduling, program build, launching and the
+  // finish (stream sync and result copies), accumulated since the last reset
+  double host_ms[2][6] = {};
+  using hclock = std::chrono::steady_clock;
+  static double ms_between(hclock::time_point a, hclock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  }
+  void host_record(int dir, const hclock::time_point (&t)[6]) {
+    host_ms[dir][0] += 1;
+    for (int k = 1; k < 6; ++k) host_ms[dir][k] += ms_between(t[k - 1], t[k]);
+  }
   int rq_prefetch = 1;      // one-state register-resident passes prefetch the next tile (QDC_RQ_PF)
   int rq_prefetch2 = 0;     // two-state ones too (QDC_RQ_PF2; 2 waves/SIMD, measured slower)
   int rq64 = 1;  // f64 gate passes register-resident too (k_rw; QDC_RQ64)
@@ -1663,6 +1675,8 @@ struct Circuit {
     return nullptr;
   }
   const char* execute(int mode, const Flat& cg, const Flat& vg, qdc_complex* out) {
+    hclock::time_point ht[6];
+    ht[0] = hclock::now();
     std::vector<size_t> gidx;
     QDC_TRY(validate_forward(cg, vg, gidx));
     QDC_TRY(dyn_reset_all());
@@ -1682,8 +1696,10 @@ struct Circuit {
           out_idx[k] = o++;
     }
     mark_inexact(cg, vg, gidx);
+    ht[1] = hclock::now();
     std::vector<qdc_plan_op> pl = plan(mode);
     std::vector<Item> items = schedule(pl, false, SIZE_MAX);
+    ht[2] = hclock::now();
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
     // a mirrored forward records what its backward will undo (forward mode only)
@@ -1694,6 +1710,7 @@ struct Circuit {
     const char* berr = build_program(items, pl, false, 0, cg, vg, gidx, mats_off, {}, 0, out_idx, nullptr);
     rec_mats = nullptr;
     QDC_TRY(berr);
+    ht[3] = hclock::now();
     if (record) {
       mrec.plan = pl;
       mrec.items = items;
@@ -1731,6 +1748,7 @@ struct Circuit {
         }
       }
     }
+    ht[4] = hclock::now();
     QDC_TRY(flush_all());
     if (record) {  // (valid once every pass ran; the backward starts from this layout)
       mrec.end_phys = layout.phys;
@@ -1743,7 +1761,10 @@ struct Circuit {
     for (auto& in : ins)
       if (is_diff_density(in.kind) || (mode == QDC_MODE_RUN && is_density(in.kind)))
         widths.push_back(is_q1_density(in.kind) ? 4 : 16);
-    return collect(sh[0].dens, widths, out);
+    QDC_TRY(collect(sh[0].dens, widths, out));
+    ht[5] = hclock::now();
+    host_record(0, ht);
+    return nullptr;
   }
 
   // D2H of `total` (>= widths.size()) result slots into host_out; the first widths.size()
@@ -1837,6 +1858,8 @@ struct Circuit {
 
   // --- backward (Circuit::backward, circuit.rs:266-429) --------------------------------------
   const char* backward(const Flat& dg, const Flat& cg, const Flat& vg, qdc_complex* out) {
+    hclock::time_point ht[6];
+    ht[0] = hclock::now();
     std::vector<size_t> gidx;
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
     QDC_TRY(dyn_reset_all());
@@ -1865,6 +1888,7 @@ struct Circuit {
     }
     bool have_bwd = false;
     mark_inexact(cg, vg, gidx);
+    ht[1] = hclock::now();
     std::vector<qdc_plan_op> pl;
     std::vector<Item> items;
     size_t first_inject = 0;
@@ -1894,10 +1918,12 @@ struct Circuit {
       items = schedule(pl, true, first_inject);
     }
     if (diag_inject) merge_diag_injections(items, pl, dg, gidx);
+    ht[2] = hclock::now();
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
                           (uint32_t)nvar, {}, &dg));
+    ht[3] = hclock::now();
     if (rq_stats)
       fprintf(stderr, "backward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
@@ -1979,6 +2005,7 @@ struct Circuit {
         have_bwd = true;
       }
     }
+    ht[4] = hclock::now();
     QDC_TRY(flush_all());
     const size_t used = nvar + stage_post.size();
     std::vector<cx*> bufs;
@@ -2020,6 +2047,8 @@ struct Circuit {
         }
       }
     }
+    ht[5] = hclock::now();
+    host_record(1, ht);
     return nullptr;
   }
 };

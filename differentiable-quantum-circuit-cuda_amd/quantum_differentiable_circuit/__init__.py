@@ -243,6 +243,16 @@ class _CircuitBase:
                                         "algo_flops": float(buf[i].algo_flops)}
                 for i in range(min(k, cap))}
 
+    def host_times(self, reset=False):
+        """Host milliseconds of this circuit's calls since the last reset (qdc_circuit_host_times):
+        {"forward" | "backward": {"calls", "setup", "schedule", "build", "launch", "finish"}}
+        ("forward" includes run calls)."""
+        buf = (C.c_double * 12)()
+        self._lib.qdc_circuit_host_times(self._h, buf, 12, 1 if reset else 0)
+        keys = ("calls", "setup", "schedule", "build", "launch", "finish")
+        return {d: {k: buf[6 * i + j] for j, k in enumerate(keys)}
+                for i, d in enumerate(("forward", "backward"))}
+
 
 def primitives_sync(precision=None):
     """Wait for the primitives' stream (qdc_abi_sync, include/qdc/dense.h)."""

@@ -30,7 +30,7 @@ RUNTIME = (
     "qdc_circuit_set_state_from_vector", "qdc_circuit_push", "qdc_circuit_len",
     "qdc_circuit_output_size", "qdc_circuit_grad_size", "qdc_circuit_execute",
     "qdc_circuit_backward", "qdc_circuit_get_state", "qdc_circuit_sync", "qdc_circuit_profile",
-    "qdc_circuit_profile_collect", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
+    "qdc_circuit_profile_collect", "qdc_circuit_host_times", "qdc_build_info", "qdc_comm_unique_id", "qdc_comm_init",
     "qdc_comm_free", "qdc_comm_allreduce", "qdc_circuit_gather_state", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
     "qdc_circuit_new_devices",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
@@ -94,6 +94,7 @@ def _proto(lib):
         "qdc_circuit_sync": (_E, [_P]),
         "qdc_circuit_profile": (_E, [_P, C.c_int]),
         "qdc_circuit_profile_collect": (_S, [_P, C.POINTER(KernelStat), _S]),
+        "qdc_circuit_host_times": (_S, [_P, C.POINTER(C.c_double), _S, C.c_int]),
         "qdc_build_info": (C.c_char_p, []),
         "qdc_comm_unique_id": (_E, [C.c_char_p]),
         "qdc_comm_init": (_E, [C.POINTER(_P), C.c_int, C.c_int, C.c_char_p]),

@@ -111,6 +111,11 @@ const char* qdc_circuit_profile(qdc_circuit* c, int on);
 /* Synchronise and aggregate the records per kernel name; returns the number of kernels
  * (writes at most `cap` entries). */
 size_t qdc_circuit_profile_collect(qdc_circuit* c, qdc_kernel_stat* out, size_t cap);
+/* Host time of the circuit's calls since the last reset (reset = 1 clears after reading):
+ * out[0..5] run / forward, out[6..11] backward, each (calls, setup ms, schedule ms, program
+ * build ms, launch ms, finish ms: stream sync, result copies, gradient reconstruction).
+ * Returns the number of values written (at most n, at most 12). */
+size_t qdc_circuit_host_times(qdc_circuit* c, double* out, size_t n, int reset);
 
 /* Library build information: "f32"/"f64", offload arch. */
 const char* qdc_build_info(void);
