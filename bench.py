@@ -374,6 +374,7 @@ def vqse_sample(steps=3):
     p = np.random.default_rng(42).normal(size=2 * layers)
     W.vqse_loss_and_grad(f, p, n, h)  # warm-up
     ac.circuit.profile(True)
+    ac.circuit.host_times(reset=True)
     t0 = time.perf_counter()
     for _ in range(steps):
         e, _ = W.vqse_loss_and_grad(f, p, n, h)
@@ -386,6 +387,8 @@ def vqse_sample(steps=3):
     avg = dom["total_ms"] / dom["launches"]
     gbs = dom["algo_bytes"] / dom["launches"] / (avg * 1e-3) / 1e9
     out["device_ms_per_call"] = round(sum(v["total_ms"] for v in stats.values()) / steps, 2)
+    out["host_ms_per_call"] = {d: {k: round(v / steps, 3) for k, v in t.items() if k != "calls"}
+                               for d, t in ac.circuit.host_times().items()}
     out["roofline"] = {"bound": "hbm", "kernel": dom_name, "achieved": round(gbs, 1),
                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                        "avg_launch_ms": round(avg, 4), "launches_per_call": dom["launches"] // steps,

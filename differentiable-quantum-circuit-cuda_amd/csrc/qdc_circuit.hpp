@@ -716,25 +716,55 @@ struct Circuit {
         pl.push_back(op);
         return (uint32_t)(pl.size() - 1);
       };
-      Item b;
-      b.type = f.type;
-      b.lc = f.lc;
-      b.h = f.h;
-      for (uint32_t r = 0; r < (uint32_t)FMAX_ROWS; ++r) b.hb[r] = f.hb[r];
-      for (auto it = f.swaps.rbegin(); it != f.swaps.rend(); ++it) b.swaps.push_back(*it);
-      if (f.type == 2) {
-        for (size_t j = f.stages.size(); j-- > 0;) {
-          std::vector<uint32_t> st;
-          for (size_t t = f.stages[j].size(); t-- > 0;) {
-            const uint32_t bi = push(f.stages[j][t]);
-            st.push_back(bi);
-            b.ops.push_back(bi);
-          }
-          b.stages.push_back(std::move(st));
-          b.mirror_of.push_back({(uint32_t)k, (uint32_t)j});
-        }
-      } else {
+      auto shell = [&]() {
+        Item b;
+        b.type = 2;
+        b.lc = f.lc;
+        b.h = f.h;
+        for (uint32_t r = 0; r < (uint32_t)FMAX_ROWS; ++r) b.hb[r] = f.hb[r];
+        return b;
+      };
+      if (f.type != 2) {
+        Item b;
+        b.type = f.type;
         b.ops.push_back(push(f.ops[0]));
+        items.push_back(std::move(b));
+        continue;
+      }
+      // the pass's densities (its last stages) become the injections that open its reverse
+      // pass (one injection pass; a single one stays a single op), then its gate stages in
+      // reverse with the forward's swaps undone in reverse order
+      size_t ng = f.stages.size();
+      while (ng > 0 && is_meas(mrec.plan[f.stages[ng - 1][0]])) --ng;
+      for (size_t j = ng; j < f.stages.size(); ++j)
+        for (uint32_t fi : f.stages[j])
+          if (!is_meas(mrec.plan[fi])) return false;  // (the planner keeps densities last)
+      if (ng < f.stages.size()) {
+        Item m = shell();
+        for (size_t j = f.stages.size(); j-- > ng;) {
+          const uint32_t bi = push(f.stages[j][0]);
+          m.ops.push_back(bi);
+          m.stages.push_back({bi});
+        }
+        if (m.ops.size() == 1) {
+          m.type = 0;
+          m.stages.clear();
+        }
+        items.push_back(std::move(m));
+      }
+      if (ng == 0) continue;
+      Item b = shell();
+      for (auto it = f.swaps.rbegin(); it != f.swaps.rend(); ++it) b.swaps.push_back(*it);
+      for (size_t j = ng; j-- > 0;) {
+        std::vector<uint32_t> st;
+        for (size_t t = f.stages[j].size(); t-- > 0;) {
+          if (is_meas(mrec.plan[f.stages[j][t]])) return false;
+          const uint32_t bi = push(f.stages[j][t]);
+          st.push_back(bi);
+          b.ops.push_back(bi);
+        }
+        b.stages.push_back(std::move(st));
+        b.mirror_of.push_back({(uint32_t)k, (uint32_t)j});
       }
       items.push_back(std::move(b));
     }

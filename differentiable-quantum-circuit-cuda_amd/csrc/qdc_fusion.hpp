@@ -88,8 +88,8 @@ struct FusionPlanner {
   // (>= NLOW; more makes the next tiles' contiguous runs longer)
   uint32_t perm_low = (uint32_t)LV + 3;
   // Mirrored schedules: the forward is scheduled so that its passes, run in reverse, are the
-  // backward's passes (qdc_circuit.hpp mirror_backward): on the two-state tile, under the
-  // ordering rules of both directions, passes of densities only or of gates only, and the
+  // backward's passes (qdc_circuit.hpp mirror_schedule): on the two-state tile, under the
+  // ordering rules of both directions, no gate after a density within a pass, and the
   // backward's cap on Gamma stages (stages holding a variable gate).  The uncompute then applies
   // exactly the adjoints of the forward's stage matrices.
   bool mirror = false;
@@ -273,6 +273,7 @@ struct FusionPlanner {
       while (!rem.empty()) {
         uint64_t mask = 0, blocked = 0;
         uint32_t nred = 0;
+        uint32_t ndens = 0;  // a mirrored forward's densities (its reduction slots)
         uint32_t left = 0;  // order classes of the ops left for a later pass
         std::vector<uint32_t> pass, rest;
         int kind = -1;  // reverse sweep: a pass is injections only or gates only
@@ -281,10 +282,16 @@ struct FusionPlanner {
           const uint64_t q = (1ull << g.pos2) | (1ull << g.pos1);
           const bool meas = is_meas(g);
           const uint32_t cls = op_class(g, backward);
-          const uint32_t isred = mfwd ? ((meas || is_var(ins[g.instr].kind)) ? 1u : 0u)
+          // (a mirrored forward: variable gates count toward the backward's Gamma cap,
+          // densities toward the forward's reduction slots)
+          const uint32_t isred = mfwd ? (is_var(ins[g.instr].kind) ? 1u : 0u)
                                  : ((!backward && meas) || (two && is_var(ins[g.instr].kind))) ? 1u : 0u;
-          if (((backward || mfwd) && kind >= 0 && (int)meas != kind) || (q & blocked) ||
-              (mfwd && meas && nred + 1 > (uint32_t)FMAX_GRAD) ||
+          // reverse sweep: a pass is injections only or gates only; a mirrored forward's pass
+          // is gates then densities (no gate after a density: its backward splits into the
+          // injections, then the gates' mirrored stages)
+          if ((backward && kind >= 0 && (int)meas != kind) || (mfwd && kind == 1 && !meas) ||
+              (q & blocked) ||
+              (mfwd && meas && ndens + 1 > (uint32_t)FMAX_GRAD) ||
               (conflicts_of(cls) & left) || pass.size() >= fuse_max_ops ||
               nred + isred > gmax || !tile_fits(mask | op_bits(g), T)) {
             blocked |= q;
@@ -295,6 +302,7 @@ struct FusionPlanner {
           pass.push_back(k);
           mask |= op_bits(g);
           nred += isred;
+          ndens += (mfwd && meas) ? 1u : 0u;
           kind = (int)meas;
         }
         // Gamma-stage cap: drop gates from the end of the pass (in pass order no kept gate

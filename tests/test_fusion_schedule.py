@@ -224,15 +224,24 @@ def test_schedule_replay_matches_sequential_oracle(monkeypatch, perturb, sched_r
     assert np.abs(final - o.state).max() < 1e-11
 
 
-def mirrored(ops_f, items_f):
+def mirrored(ops_f, items_f, ins):
     """The backward schedule QDC_MIRROR runs (qdc_circuit.hpp mirror_schedule): the forward's
-    passes in reverse, stages and the ops in them reversed.  Forward plan index i is backward
-    plan index L - 1 - i (both plans hold the gates and differentiable densities)."""
+    passes in reverse, stages and the ops in them reversed; a pass's trailing densities become
+    the injections that open its reverse pass (one item).  Forward plan index i is backward plan
+    index L - 1 - i (both plans hold the gates and differentiable densities)."""
     L = len(ops_f)
     items = []
     for it in reversed(items_f):
-        st = [[L - 1 - i for i in reversed(s)] for s in reversed(it["stages"])]
-        items.append(dict(it, stages=st))
+        stages = it["stages"]
+        ng = len(stages)
+        while ng and ins[ops_f[stages[ng - 1][0]]["instr"]][0] in DENS:
+            ng -= 1
+        if ng < len(stages):
+            st = [[L - 1 - s[0]] for s in reversed(stages[ng:])]
+            items.append(dict(it, type=2 if len(st) > 1 else 0, stages=st))
+        if ng:
+            st = [[L - 1 - i for i in reversed(s)] for s in reversed(stages[:ng])]
+            items.append(dict(it, stages=st))
     return ops_f[::-1], items
 
 
@@ -241,23 +250,24 @@ def mirrored(ops_f, items_f):
 @pytest.mark.parametrize("n,seed,perturb", [(14, 1, 0.0), (17, 2, 1e-3), (24, 3, 0.0)])
 def test_mirrored_schedule_invariants(monkeypatch, prec, sched_rq, n, seed, perturb):
     """QDC_MIRROR: the forward is scheduled on the two-state tile so that its passes run in
-    reverse are a valid reverse sweep - the invariants of both directions hold, passes are
-    densities only or gates only, none spans the last differentiable density, and the Gamma
-    stages (stages holding a variable gate) of a pass fit the 16 accumulators."""
+    reverse are a valid reverse sweep - the invariants of both directions hold, none spans the
+    last differentiable density, and the Gamma
+    stages (stages holding a variable gate) of a pass fit the 16 accumulators; a pass holds gate
+    stages, then densities."""
     monkeypatch.setenv("QDC_SCHED_RQ", sched_rq)
     monkeypatch.setenv("QDC_SCHED_MIRROR", "1")
     ins, const, var, gates, sens = make(n, seed, perturb)
     ops_f, items_f = schedule(n, ins, 1, sens, prec)
     perm = sched_rq == "1"
     check_invariants(n, ins, sens, 1, prec, ops_f, items_f, permuted=perm, tbits=T[2])
-    ops_b, items_b = mirrored(ops_f, items_f)
+    ops_b, items_b = mirrored(ops_f, items_f, ins)
     check_invariants(n, ins, sens, 2, prec, ops_b, items_b, permuted=perm, tbits=T[2])
     var_kinds = set(Q1 + Q2 + DIAG) - set(CONST)
     for it in items_f:
         if it["type"] != 2:
             continue
-        members = [i for st in it["stages"] for i in st]
-        assert len({ins[ops_f[i]["instr"]][0] in DENS for i in members}) == 1
+        meas = [ins[ops_f[st[0]]["instr"]][0] in DENS for st in it["stages"]]
+        assert meas == sorted(meas)  # gate stages, then densities
         gst = sum(any(ins[ops_f[i]["instr"]][0] in var_kinds for i in st) for st in it["stages"])
         assert gst <= 16
     assert sum(it["type"] == 2 for it in items_f) > 3
@@ -273,7 +283,7 @@ def test_mirrored_schedule_replay_matches_sequential_oracle(monkeypatch, sched_r
     ins, const, var, gates, sens = make(n, 11, 1e-3)
     ops, items = {}, {}
     ops["fwd"], items["fwd"] = schedule(n, ins, 1, sens, "f32")
-    ops["bwd"], items["bwd"] = mirrored(ops["fwd"], items["fwd"])
+    ops["bwd"], items["bwd"] = mirrored(ops["fwd"], items["fwd"], ins)
     assert sum(it["type"] == 2 for it in items["fwd"]) > 3
     psi0 = O.random_state(np.random.default_rng(5), n)
     o = O.OracleCircuit(n)

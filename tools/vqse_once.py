@@ -9,5 +9,5 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 import bench  # noqa: E402
 
 r = bench.vqse_sample()
-print(json.dumps({k: r[k] for k in ("s_per_loss_grad_call", "energy", "device_ms_per_call")}),
+print(json.dumps({k: r[k] for k in ("s_per_loss_grad_call", "energy", "device_ms_per_call", "host_ms_per_call")}),
       json.dumps(r.get("roofline")), flush=True)
