@@ -1022,7 +1022,8 @@ struct Circuit {
         const uint32_t lo = (uint32_t)__builtin_ctzll(qm);
         const uint32_t hi = 63u - (uint32_t)__builtin_clzll(qm);
         const int R = lo == hi ? 2 : 4;
-        SMat A = smat_identity(R), B = smat_identity(R);
+        SMat A = smat_identity(R);
+        SMatD B = smat_identity<double>(R);
         StagePost post;
         post.R = R;
         post.diag_only = all_diag;
@@ -1040,13 +1041,14 @@ struct Circuit {
             role = op.pos2 == hi ? ROLE_Q2 : ROLE_Q2_SWAP;
           // the applied matrix a (forward: U; uncompute: U^dagger / U^-1 / conj diagonal) and
           // the pull-back b = U^T (diagonal: d), each in the gate's own basis
-          cd ga[16], gb[16];
+          cd ga[16];
+          cdd gb[16];
           if (dg) {
             const diag4 d = to_diag(g4);
             const diag4 a = backward ? conj_diag(d) : d;
             for (int i = 0; i < 4; ++i) {
               ga[i] = cd(a.a[i].x, a.a[i].y);
-              gb[i] = cd(d.a[i].x, d.a[i].y);
+              gb[i] = cdd(d.a[i].x, d.a[i].y);
             }
           } else if (is_q1_gate(in.kind)) {
             const mat<2> u = to_mat<2>(g4);
@@ -1060,7 +1062,7 @@ struct Circuit {
             const mat<2> bt = transpose<2>(u);
             for (int i = 0; i < 4; ++i) {
               ga[i] = cd(a.a[i].x, a.a[i].y);
-              gb[i] = cd(bt.a[i].x, bt.a[i].y);
+              gb[i] = cdd(bt.a[i].x, bt.a[i].y);
             }
           } else {
             const mat<4> u = to_mat<4>(g4);
@@ -1074,13 +1076,14 @@ struct Circuit {
             const mat<4> bt = transpose<4>(u);
             for (int i = 0; i < 16; ++i) {
               ga[i] = cd(a.a[i].x, a.a[i].y);
-              gb[i] = cd(bt.a[i].x, bt.a[i].y);
+              gb[i] = cdd(bt.a[i].x, bt.a[i].y);
             }
           }
-          const SMat Ea = stage_embed(ga, dg, role, R), Eb = stage_embed(gb, dg, role, R);
+          const SMat Ea = stage_embed(ga, dg, role, R);
+          const SMatD Eb = stage_embed(gb, dg, role, R);
           const SMat Anew = smat_mul(Ea, A);
           if (two && is_var(in.kind))
-            post.gates.push_back(StageGate{var_idx[op.instr], dg, role, B, smat_transpose(Anew)});
+            post.gates.push_back(StageGate{var_idx[op.instr], dg, role, B, smat_double(smat_transpose(Anew))});
           A = Anew;
           B = smat_mul(Eb, B);
         }
@@ -1135,7 +1138,7 @@ struct Circuit {
         const int n = all_diag ? 4 : R * R;
         for (int i = 0; i < n; ++i) {
           const cd va = all_diag ? Aup.a[i * 4 + i] : Aup.a[i];
-          const cd vb = all_diag ? B.a[i * 4 + i] : B.a[i];
+          const cdd vb = all_diag ? B.a[i * 4 + i] : B.a[i];
           mats[mo + i] = cx{(real)va.real(), (real)va.imag()};
           mats[mo + n + i] = cx{(real)vb.real(), (real)vb.imag()};
         }
@@ -2050,24 +2053,24 @@ struct Circuit {
       std::vector<size_t> off(widths.size() + 1, 0);
       for (size_t j = 0; j < widths.size(); ++j) off[j + 1] = off[j] + widths[j];
       for (const StagePost& st : stage_post) {
-        SMat G = smat_identity(st.R);
+        SMatD G = smat_identity<double>(st.R);
         const cx* g = host_out + (size_t)st.slot * RED;
         auto sw = [&](int p) { return st.swapped ? swap_bits4(p) : p; };
         if (st.diag_only) {
           for (int i = 0; i < 16; ++i) G.a[i] = 0;
-          for (int r = 0; r < 4; ++r) G.a[r * 4 + r] = cd(g[sw(r)].x, g[sw(r)].y);
+          for (int r = 0; r < 4; ++r) G.a[r * 4 + r] = cdd(g[sw(r)].x, g[sw(r)].y);
         } else if (st.R == 4) {
           for (int p = 0; p < 4; ++p)
             for (int q = 0; q < 4; ++q) {
               const cx v = g[sw(p) * 4 + sw(q)];
-              G.a[p * 4 + q] = cd(v.x, v.y);
+              G.a[p * 4 + q] = cdd(v.x, v.y);
             }
         } else {
-          for (int i = 0; i < st.R * st.R; ++i) G.a[i] = cd(g[i].x, g[i].y);
+          for (int i = 0; i < st.R * st.R; ++i) G.a[i] = cdd(g[i].x, g[i].y);
         }
         for (const StageGate& sg : st.gates) {
-          const SMat M = smat_mul(smat_mul(sg.L, G), sg.Rt);
-          cd v[16];
+          const SMatD M = smat_mul(smat_mul(sg.L, G), sg.Rt);
+          cdd v[16];
           stage_extract(M, sg.diag, sg.role, v);
           qdc_complex* o = out + off[sg.var];
           for (int k = 0; k < widths[sg.var]; ++k) {

@@ -30,41 +30,59 @@ using hreal = long double;
 #else
 using hreal = double;
 #endif
-using cd = std::complex<hreal>;
 
-struct SMat {  // R x R, row-major, R = 2 or 4
+template <class T>
+struct SMatT {  // R x R, row-major, R = 2 or 4
   int R = 4;
-  cd a[16];
+  std::complex<T> a[16];
 };
+// A: the products applied to the state (forward and uncompute), in the wide type; D: the
+// pull-back products and the gradient reconstruction, in double (their rounding stays within
+// the reference's floors in both precisions, tests/floors.py)
+using SMat = SMatT<hreal>;
+using SMatD = SMatT<double>;
+using cd = std::complex<hreal>;
+using cdd = std::complex<double>;
 
-inline SMat smat_identity(int R) {
-  SMat m;
+template <class T = hreal>
+inline SMatT<T> smat_identity(int R) {
+  SMatT<T> m;
   m.R = R;
   for (int i = 0; i < R * R; ++i) m.a[i] = 0;
   for (int i = 0; i < R; ++i) m.a[i * R + i] = 1;
   return m;
 }
-inline SMat smat_mul(const SMat& x, const SMat& y) {
-  SMat z;
+template <class T>
+inline SMatT<T> smat_mul(const SMatT<T>& x, const SMatT<T>& y) {
+  SMatT<T> z;
   z.R = x.R;
   const int R = x.R;
   for (int p = 0; p < R; ++p)
     for (int q = 0; q < R; ++q) {
-      hreal sr = 0, si = 0;  // (real arithmetic: no complex-multiply NaN/Inf recovery path)
+      T sr = 0, si = 0;  // (real arithmetic: no complex-multiply NaN/Inf recovery path)
       for (int k = 0; k < R; ++k) {
-        const cd u = x.a[p * R + k], v = y.a[k * R + q];
+        const std::complex<T> u = x.a[p * R + k], v = y.a[k * R + q];
         sr += u.real() * v.real() - u.imag() * v.imag();
         si += u.real() * v.imag() + u.imag() * v.real();
       }
-      z.a[p * R + q] = cd(sr, si);
+      z.a[p * R + q] = std::complex<T>(sr, si);
     }
   return z;
 }
-inline SMat smat_transpose(const SMat& x) {
-  SMat z;
+template <class T>
+inline SMatT<T> smat_transpose(const SMatT<T>& x) {
+  SMatT<T> z;
   z.R = x.R;
   for (int p = 0; p < x.R; ++p)
     for (int q = 0; q < x.R; ++q) z.a[p * x.R + q] = x.a[q * x.R + p];
+  return z;
+}
+// the same matrix in double
+template <class T>
+inline SMatD smat_double(const SMatT<T>& x) {
+  SMatD z;
+  z.R = x.R;
+  for (int i = 0; i < x.R * x.R; ++i) z.a[i] = cdd((double)x.a[i].real(), (double)x.a[i].imag());
   return z;
 }
 
@@ -82,8 +100,9 @@ enum StageRole : int {
 
 // Embed a gate's matrix (its own basis; R_g = 2 or 4 entries row-major, or a diagonal of 4 when
 // `diag`) into the stage basis of dimension R.
-inline SMat stage_embed(const cd* g, bool diag, int role, int R) {
-  SMat m = smat_identity(R);
+template <class T>
+inline SMatT<T> stage_embed(const std::complex<T>* g, bool diag, int role, int R) {
+  SMatT<T> m = smat_identity<T>(R);
   if (role == ROLE_Q1_ONLY) {
     for (int i = 0; i < 4; ++i) m.a[i] = g[i];
     return m;
@@ -94,9 +113,9 @@ inline SMat stage_embed(const cd* g, bool diag, int role, int R) {
       for (int c = 0; c < 4; ++c) {
         const int rh = r >> 1, rl = r & 1, ch = c >> 1, cl = c & 1;
         if (role == ROLE_Q1_LO)
-          m.a[r * 4 + c] = (rh == ch) ? g[rl * 2 + cl] : cd(0);
+          m.a[r * 4 + c] = (rh == ch) ? g[rl * 2 + cl] : std::complex<T>(0);
         else
-          m.a[r * 4 + c] = (rl == cl) ? g[rh * 2 + ch] : cd(0);
+          m.a[r * 4 + c] = (rl == cl) ? g[rh * 2 + ch] : std::complex<T>(0);
       }
     return m;
   }
@@ -114,7 +133,7 @@ inline SMat stage_embed(const cd* g, bool diag, int role, int R) {
 
 // Gradient of one gate (its own index order) from M = L Gamma Rt in the stage basis.
 // Writes 4 (q1, diagonal) or 16 (two-qubit) complex values.
-inline void stage_extract(const SMat& M, bool diag, int role, cd* out) {
+inline void stage_extract(const SMatD& M, bool diag, int role, cdd* out) {
   if (role == ROLE_Q1_ONLY) {
     for (int i = 0; i < 4; ++i) out[i] = M.a[i];
     return;
@@ -122,7 +141,7 @@ inline void stage_extract(const SMat& M, bool diag, int role, cd* out) {
   if (role == ROLE_Q1_LO || role == ROLE_Q1_HI) {
     for (int i = 0; i < 2; ++i)
       for (int j = 0; j < 2; ++j) {
-        cd s = 0;
+        cdd s = 0;
         for (int k = 0; k < 2; ++k) {
           const int r = role == ROLE_Q1_LO ? 2 * k + i : 2 * i + k;
           const int c = role == ROLE_Q1_LO ? 2 * k + j : 2 * j + k;
@@ -152,7 +171,7 @@ struct StageGate {
   uint32_t var;  // row of the gradient output (variable-gate order)
   bool diag;
   int role;
-  SMat L, Rt;  // G_stage = L Gamma Rt
+  SMatD L, Rt;  // G_stage = L Gamma Rt
 };
 
 // A stage whose Gamma is reduced into gradient slot `slot`.
