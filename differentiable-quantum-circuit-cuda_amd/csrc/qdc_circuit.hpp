@@ -284,8 +284,9 @@ struct Circuit {
   // the O(1)-memory uncompute then drifts like the reference's gate-by-gate U, U^dagger sequence
   // instead of accumulating the rounding of independently formed stage products.  Unsharded
   // circuits; the backward must follow a forward call with the same gates (else the backward
-  // schedules itself as usual).
-  int mirror = 0;
+  // schedules itself as usual).  On by default (round 4: C5 n = 14 f32 uncompute 4.85x -> 1.4x
+  // the reference's floor; C2 n = 28 f32 ~3.5 % slower, DESIGN.md "Uncompute drift").
+  int mirror = 1;
   bool mirror_on() const {
     return mirror && g == 0 && fuse && fuse_max_ops >= 2 && use_rq && (sizeof(real) == 4 || rq64);
   }
@@ -786,7 +787,7 @@ struct Circuit {
     P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
     P.tile1_chunks = tile1_chunks;
-    P.mirror = mirror_on();
+    P.mirror = mirror_on() && sched_mirror;
     P.gamma_stage_cap = rq_gstage != 0;
     return P;
   }
@@ -808,11 +809,15 @@ struct Circuit {
   struct SchedCache {
     bool valid = false;
     size_t first_inject = 0;
+    bool mirror = false;
     std::vector<qdc_plan_op> in_plan, out_plan;
     std::vector<uint8_t> inexact;
     std::vector<Item> items;
   };
   SchedCache sched_cache[2];  // forward / run, backward
+  // the schedule being built is a mirrored forward's (forward calls only: a run call has no
+  // backward to mirror and keeps the one-state schedule)
+  bool sched_mirror = false;
   int sched_cache_on = 1;
   static bool same_plan(const std::vector<qdc_plan_op>& a, const std::vector<qdc_plan_op>& b) {
     if (a.size() != b.size()) return false;
@@ -829,7 +834,7 @@ struct Circuit {
   std::vector<Item> schedule(std::vector<qdc_plan_op>& plan, bool backward, size_t first_inject) {
     SchedCache& c = sched_cache[backward ? 1 : 0];
     if (sched_cache_on && c.valid && c.first_inject == first_inject && c.inexact == inexact &&
-        same_plan(c.in_plan, plan)) {
+        c.mirror == sched_mirror && same_plan(c.in_plan, plan)) {
       plan = c.out_plan;
       return c.items;
     }
@@ -841,6 +846,7 @@ struct Circuit {
       c.items = items;
       c.inexact = inexact;
       c.first_inject = first_inject;
+      c.mirror = sched_mirror;
       c.valid = true;
     }
     return items;
@@ -1466,7 +1472,8 @@ struct Circuit {
       return ctx.launch_block(name, bytes, k_rw<false, 2, true, 1, true>, grid, 64u, f, b, fops,
                               mats, g, l0, partials, stride);
     }
-    if ((two ? (rq_wave & 1) : rw1()) && (nt == 128 || (nt == 256 && !two))) {
+    if ((two ? (rq_wave & 1) : ((rq_wave & 2) || (rw1() && nt == 128))) &&
+        (nt == 128 || (nt == 256 && !two))) {
       // k_rw: lane l of a tile's W waves runs k_rq's threads l + 64 W e (e < 2)
       const bool pfw = two && (rq_wave & 4);
       const uint32_t bs = (!two && nt == 256) ? 128u : 64u;
@@ -1731,6 +1738,7 @@ struct Circuit {
     mark_inexact(cg, vg, gidx);
     ht[1] = hclock::now();
     std::vector<qdc_plan_op> pl = plan(mode);
+    sched_mirror = mode == QDC_MODE_FORWARD;
     std::vector<Item> items = schedule(pl, false, SIZE_MAX);
     ht[2] = hclock::now();
     size_t mats_off = 0;

@@ -266,14 +266,21 @@ inline bool spec_source_fp(const std::string& csrc, const std::string& inc, uint
 }
 
 // the library's own compile-time switches, so the kernels agree with it
+#ifndef QDC_NT_LOAD
+#define QDC_NT_LOAD 1
+#endif
+#ifndef QDC_NT_STORE
+#define QDC_NT_STORE 1
+#endif
 inline std::string spec_defines() {
   char b[512];
   snprintf(b, sizeof b,
            "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
-           "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d%s",
+           "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d "
+           "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d%s",
            (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
            (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-           sizeof(real) == 8 ? " -DQDC_F64" : "");
+           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, sizeof(real) == 8 ? " -DQDC_F64" : "");
   return b;
 }
 // hipcc options of every specialized kernel besides the defines and include paths

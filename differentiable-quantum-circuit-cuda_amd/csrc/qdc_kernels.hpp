@@ -72,13 +72,28 @@ struct diag4 {
 // Every state lives in global memory: the accesses go through address space 1, so they stay
 // global_load/store even where a laundered pointer (asm "+v") lost the address space
 // (flat_* would also count in lgkmcnt and complete out of order).
+// (QDC_NT_LOAD / QDC_NT_STORE = 0: plain accesses, for A/B builds, tools/build_variant.sh)
+#ifndef QDC_NT_LOAD
+#define QDC_NT_LOAD 1
+#endif
+#ifndef QDC_NT_STORE
+#define QDC_NT_STORE 1
+#endif
 typedef __attribute__((address_space(1))) vec16 gvec16;
 __device__ __forceinline__ chunk ldc(const chunk* p) {
+#if QDC_NT_LOAD
   const vec16 v = __builtin_nontemporal_load((const gvec16*)(p));
+#else
+  const vec16 v = *(const gvec16*)(p);
+#endif
   return __builtin_bit_cast(chunk, v);
 }
 __device__ __forceinline__ void stc(chunk* p, const chunk& c) {
+#if QDC_NT_STORE
   __builtin_nontemporal_store(__builtin_bit_cast(vec16, c), (gvec16*)(p));
+#else
+  *(gvec16*)(p) = __builtin_bit_cast(vec16, c);
+#endif
 }
 
 __device__ __forceinline__ cx cmul(cx a, cx b) {

@@ -249,9 +249,11 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   const char* ew = getenv("QDC_QK_WIDE");
   bool wide = ew ? atoi(ew) != 0 : k >= 4;
   // software-pipelined batches (k_qk PF; knob QDC_QK_PF=0/1): NB batches in flight while the
-  // previous NB run on the matrix cores — replaces "wide" (same registers)
+  // previous NB run on the matrix cores — replaces "wide" (same registers).  Measured at n = 28
+  // (tools/qk_probe.py --pf, profiles/r4i_qk_pf_ab.log): k = 3 0.643 -> 0.676, k = 5 0.515 ->
+  // 0.562 of HBM, k = 4 0.573 -> 0.568; on by default at k = 3, 5
   const char* epf = getenv("QDC_QK_PF");
-  const bool pf = epf ? atoi(epf) != 0 : false;
+  const bool pf = epf ? atoi(epf) != 0 : k != 4;
   if (pf) wide = false;
   const uint64_t nb = (k == 3 ? 4 : k == 4 ? 2 : 1) * (wide ? 2 : 1);
   const uint64_t gpb = pair ? 32 : 16;  // groups per batch
