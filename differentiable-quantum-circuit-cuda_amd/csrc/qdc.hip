@@ -460,6 +460,7 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   if (const char* e = getenv("QDC_SCHED_RQ")) P.permute = P.rq_grad = atoi(e) != 0;
   if (const char* e = getenv("QDC_SCHED_PERM")) P.permute = atoi(e) != 0;  // f64: rq_grad only
   if (const char* e = getenv("QDC_SCHED_MIRROR")) P.mirror = atoi(e) != 0;  // QDC_MIRROR's forward
+  if (const char* e = getenv("QDC_DEFER_Q1")) P.defer_q1 = atoi(e) != 0;
   if (const char* e = getenv("QDC_RQ_PERM_LOW")) P.perm_low = (uint32_t)atoi(e);
   if (const char* e = getenv("QDC_RQ_GSTAGE")) P.gamma_stage_cap = atoi(e) != 0;
   std::vector<qdc_plan_op> pl(plan, plan + n_plan);

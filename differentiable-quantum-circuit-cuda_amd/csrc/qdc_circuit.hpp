@@ -287,6 +287,9 @@ struct Circuit {
   // schedules itself as usual).  On by default (round 4: C5 n = 14 f32 uncompute 4.85x -> 1.4x
   // the reference's floor; C2 n = 28 f32 ~3.5 % slower, DESIGN.md "Uncompute drift").
   int mirror = 1;
+  // trailing one-qubit stages of a pass join their qubit's next two-qubit stage in a later pass
+  // (qdc_fusion.hpp defer_trailing_q1; QDC_DEFER_Q1)
+  int defer_q1 = 1;
   bool mirror_on() const {
     return mirror && g == 0 && fuse && fuse_max_ops >= 2 && use_rq && (sizeof(real) == 4 || rq64);
   }
@@ -358,6 +361,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
     if (const char* e = getenv("QDC_MIRROR")) mirror = atoi(e);
+    if (const char* e = getenv("QDC_DEFER_Q1")) defer_q1 = atoi(e);
     if (const char* e = getenv("QDC_SCHED_CACHE")) sched_cache_on = atoi(e);
     if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
       const uint32_t t = (uint32_t)atoi(e);
@@ -788,6 +792,7 @@ struct Circuit {
     if (rq_perm_low) P.perm_low = rq_perm_low;
     P.tile1_chunks = tile1_chunks;
     P.mirror = mirror_on() && sched_mirror;
+    P.defer_q1 = defer_q1 != 0;
     P.gamma_stage_cap = rq_gstage != 0;
     return P;
   }

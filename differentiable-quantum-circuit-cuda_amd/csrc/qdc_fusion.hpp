@@ -93,6 +93,9 @@ struct FusionPlanner {
   // backward's cap on Gamma stages (stages holding a variable gate).  The uncompute then applies
   // exactly the adjoints of the forward's stage matrices.
   bool mirror = false;
+  // trailing one-qubit stages move to the pass of their qubit's next two-qubit gate
+  // (defer_trailing_q1; QDC_DEFER_Q1)
+  bool defer_q1 = true;
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -320,6 +323,10 @@ struct FusionPlanner {
             for (uint32_t k : pass) mask |= op_bits(plan[k]);
           }
         }
+        if (defer_q1 && defer_trailing_q1(pass, rest, plan, backward)) {
+          mask = 0;
+          for (uint32_t k : pass) mask |= op_bits(plan[k]);
+        }
         if (pass.size() == 1) {
           items.push_back(FusionItem{0, pass});
         } else {
@@ -335,6 +342,61 @@ struct FusionPlanner {
       i = j;
     }
     return items;
+  }
+
+  // A stage of one-qubit gates that ends its qubit's run in a pass, when that qubit's next op
+  // (left for a later pass) is a two-qubit gate, moves to the later pass: there it joins the
+  // two-qubit gate's stage instead of costing a stage of its own (2 complex MACs per amplitude
+  // forward, 6 in the reverse sweep).  Only stages no later op of the pass depends on (shared
+  // qubit or conflicting order classes) move; at least one stage stays.  Returns whether any
+  // moved (rest stays in plan order).
+  bool defer_trailing_q1(std::vector<uint32_t>& pass, std::vector<uint32_t>& rest,
+                         const std::vector<qdc_plan_op>& plan, bool backward) const {
+    if (pass.size() < 2 || rest.empty()) return false;
+    const std::vector<std::vector<uint32_t>> sts = stage_partition(pass, plan, backward);
+    if (sts.size() < 2) return false;
+    std::vector<uint32_t> moved;
+    size_t kept_stages = sts.size();
+    for (const auto& st : sts) {
+      if (kept_stages <= 1) break;
+      // (one-qubit gates on one qubit only)
+      bool q1only = true;
+      for (uint32_t k : st)
+        q1only = q1only && is_gate_op(plan[k]) && plan[k].pos2 == plan[k].pos1 &&
+                 plan[k].pos2 == plan[st[0]].pos2;
+      if (!q1only) continue;
+      const uint32_t qb = plan[st[0]].pos2;
+      const uint64_t qm = 1ull << qb;
+      bool free = true;  // no later op of the pass depends on the stage
+      for (uint32_t x : st) {
+        const uint32_t cx = op_class(plan[x], backward);
+        for (uint32_t y : pass) {
+          if (y <= x || std::find(st.begin(), st.end(), y) != st.end()) continue;
+          if (std::find(moved.begin(), moved.end(), y) != moved.end()) continue;
+          const uint64_t yq = (1ull << plan[y].pos2) | (1ull << plan[y].pos1);
+          if ((yq & qm) || (conflicts_of(cx) & op_class(plan[y], backward))) free = false;
+        }
+      }
+      if (!free) continue;
+      // the qubit's next op in the rest of the window: a two-qubit gate
+      const qdc_plan_op* next = nullptr;
+      for (uint32_t k : rest)
+        if (k > st.back() && (((1ull << plan[k].pos2) | (1ull << plan[k].pos1)) & qm)) {
+          next = &plan[k];
+          break;
+        }
+      if (!next || !is_gate_op(*next) || next->pos2 == next->pos1) continue;
+      moved.insert(moved.end(), st.begin(), st.end());
+      --kept_stages;
+    }
+    if (moved.empty()) return false;
+    std::vector<uint32_t> keep;
+    for (uint32_t k : pass)
+      if (std::find(moved.begin(), moved.end(), k) == moved.end()) keep.push_back(k);
+    pass.swap(keep);
+    rest.insert(rest.end(), moved.begin(), moved.end());
+    std::sort(rest.begin(), rest.end());
+    return true;
   }
 
   uint32_t gamma_stages(const std::vector<uint32_t>& pass, const std::vector<qdc_plan_op>& plan,

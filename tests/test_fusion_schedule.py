@@ -302,3 +302,25 @@ def test_mirrored_schedule_replay_matches_sequential_oracle(monkeypatch, sched_r
     ga, gb = np.concatenate(got_g), np.concatenate(want_g)
     assert np.abs(ga - gb).max() < 1e-11 * np.abs(gb).max()
     assert np.abs(final - o.state).max() < 1e-11
+
+
+@pytest.mark.parametrize("mirror", ["0", "1"])
+def test_trailing_one_qubit_stages_join_the_next_pass(monkeypatch, mirror):
+    """C2's generator at n = 28 (20 layers) on the runtime's f32 settings: a stage of one-qubit
+    gates left at the end of a pass moves to the pass of its qubit's next two-qubit gate
+    (defer_trailing_q1), so almost every one-qubit gate shares a two-qubit gate's stage — the
+    minimum is one stage per two-qubit gate (540)."""
+    from quantum_differentiable_circuit import workloads as W
+    monkeypatch.setenv("QDC_SCHED_RQ", "1")
+    monkeypatch.setenv("QDC_SCHED_MIRROR", mirror)
+    n = 28
+    ins, _ = W.layered_circuit(n, 20, 1)
+    stages = {}
+    for defer in ("0", "1"):
+        monkeypatch.setenv("QDC_DEFER_Q1", defer)
+        ops, items = schedule(n, ins, 2 if mirror == "0" else 1, [0] * len(ins), "f32")
+        check_invariants(n, ins, [0] * len(ins), 2 if mirror == "0" else 1, "f32", ops, items,
+                         permuted=True, tbits=T[2])
+        stages[defer] = sum(1 for it in items if it["type"] == 2 for s in it["stages"]
+                            if ins[ops[s[0]]["instr"]][0] not in DENS)
+    assert stages["1"] <= 542 and stages["1"] <= stages["0"], stages

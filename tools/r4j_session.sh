@@ -10,7 +10,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --time
   --deselect tests/test_gpu_drift.py::test_c5_full_size_10k_gates > "$OUT/tests.log" 2>&1
 rc=$?; grep -E "passed|failed|error" "$OUT/tests.log" | tail -2; [ $rc -eq 0 ] || exit $rc
 grep -c "passes-by ATOL" "$OUT/tests.log"
-TAG=${TAG:-r4j}/ab REPS=2 STEPS_N=5 CFGS="- QDC_MIRROR=0" bash tools/ab_env.sh || exit $?
+TAG=${TAG:-r4j}/ab REPS=2 STEPS_N=5 CFGS="- QDC_MIRROR=0 QDC_DEFER_Q1=0" bash tools/ab_env.sh || exit $?
 for v in lib exp/ntld0 exp/ntst0 exp/nt00; do
   if [ $v = lib ]; then d=""; else d="$PWD/$v"; fi
   tag=$(echo $v | tr '/' '_')
