@@ -419,8 +419,8 @@ inline uint32_t per_thread(uint64_t items, uint32_t target) {
 
 // q1: R = 2, pos2 == pos1 == target.  q2: R = 4.
 inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_states,
-                      uint32_t grid_target, bool far_tile = false, bool wide2 = false,
-                      bool wide1 = false) {
+                      uint32_t grid_target, bool far_tile = false, uint32_t wide2 = 0,
+                      uint32_t wide1 = 0) {
   Plan p;
   p.R = R;
   const uint64_t nch = nchunks_of(n);
@@ -458,8 +458,9 @@ inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_
   }
   // TILE: 256*K chunks per state per tile, K = 4 (one state) or 2 (two states)
   p.tile = true;
-  // wide2: two-state tiles of 2^10 chunks; wide1: one-state tiles of 2^11
-  const uint32_t T = two_states ? (wide2 ? 10 : 9) : (wide1 ? 11 : 10);
+  // wide2: two-state tiles of 2^(9 + wide2) chunks; wide1: one-state tiles of 2^(10 + wide1)
+  // (wide = 2: 64 KiB of LDS per block)
+  const uint32_t T = two_states ? 9 + (wide2 > 2 ? 2 : wide2) : 10 + (wide1 > 2 ? 2 : wide1);
   const uint32_t cbits = log2u(nch);
   const uint32_t teff = cbits < T ? cbits : T;
   // targets at chunk bits beyond the tile's contiguous bits become row bits (each row bit
@@ -604,8 +605,12 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
   const uint32_t grid = blocks_of(p);
   if (p.tile) {
     constexpr int K = op_two_states(OP) ? 2 : 4;
+    if (K == 2 && p.tg.l + p.tg.h > 10)  // the widest two-state tile (QDC_TILE2_WIDE=2)
+      return c.launch(name, bytes, k_tile<OP, R, 8>, grid, fc, bc, A, B, p.tg, partials);
     if (K == 2 && p.tg.l + p.tg.h > 9)  // a wide two-state tile (QDC_TILE2_WIDE)
       return c.launch(name, bytes, k_tile<OP, R, 4>, grid, fc, bc, A, B, p.tg, partials);
+    if (K == 4 && p.tg.l + p.tg.h > 11)  // the widest one-state tile (QDC_TILE1_WIDE=2)
+      return c.launch(name, bytes, k_tile<OP, R, 16>, grid, fc, bc, A, B, p.tg, partials);
     if (K == 4 && p.tg.l + p.tg.h > 10)  // a wide one-state tile (QDC_TILE1_WIDE)
       return c.launch(name, bytes, k_tile<OP, R, 8>, grid, fc, bc, A, B, p.tg, partials);
     return c.launch(name, bytes, k_tile<OP, R, K>, grid, fc, bc, A, B, p.tg, partials);
@@ -626,7 +631,7 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
                      bool reduces, bool writes_both = false) {
   const uint32_t cls = writes_both ? 0u : two ? 2u : 1u;  // QDC_TILE_FAR bit
   Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
-                     (c.tile_far >> cls) & 1u, c.tile2_wide != 0, c.tile1_wide != 0);
+                     (c.tile_far >> cls) & 1u, c.tile2_wide, c.tile1_wide);
   if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   // XCD-aware order for streaming launches only by default: reductions (few long-lived blocks
   // with contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)

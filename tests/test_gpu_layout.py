@@ -98,16 +98,20 @@ def test_far_target_tile_plans(prec):
     psi0 = O.random_state(np.random.default_rng(8), n)
     fl = F.Floor(prec, n, ins, const, var, psi0=psi0, cots=F.tsallis_cots, run=False)
     res = {}
-    for tf in (0, 7):
-        old = os.environ.get("QDC_TILE_FAR")
-        os.environ["QDC_TILE_FAR"] = str(tf)
+    # 7w: every class tiled on the widest tiles (QDC_TILE{1,2}_WIDE=2: 2^12 / 2^11 chunks)
+    knobs = {0: {"QDC_TILE_FAR": "0"}, 7: {"QDC_TILE_FAR": "7"},
+             "7w": {"QDC_TILE_FAR": "7", "QDC_TILE1_WIDE": "2", "QDC_TILE2_WIDE": "2"}}
+    for tf, kv in knobs.items():
+        old = {k: os.environ.get(k) for k in kv}
+        os.environ.update(kv)
         try:
             c = build(prec, n, ins, 1, fuse=0)
         finally:
-            if old is None:
-                del os.environ["QDC_TILE_FAR"]
-            else:
-                os.environ["QDC_TILE_FAR"] = old
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
         c.set_state_from_vector(fl.psi0)
         d = c.forward(fl.const, fl.var)
         fwd = c.get_state(0)
@@ -120,3 +124,4 @@ def test_far_target_tile_plans(prec):
         res[tf] = g
         del c
     F.check_pair(prec, res[7], res[0], fl.floor["grads"], f"n={n} {prec} tiled vs direct grads")
+    F.check_pair(prec, res["7w"], res[0], fl.floor["grads"], f"n={n} {prec} wide tiles vs direct grads")
