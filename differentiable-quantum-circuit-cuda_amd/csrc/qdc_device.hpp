@@ -128,9 +128,11 @@ struct Ctx {
   // bits) instead of the direct rows.  Knob QDC_TILE_FAR, one bit per op class: bit 0 reverse
   // (both states read and written), bit 1 one-state ops, bit 2 inject / grad.  Measured at
   // n = 28 (profiles/r2m_micro_table_tf*.txt): reverse_q1 68-70 -> 75-77 % of 8 TB/s at every
-  // far position, reverse_q2 (14,13) 65.7 -> 69.6 %; one-state apply 77 -> 68 % and inject
-  // 79 -> 71 % at some positions, so only bit 0 is on
-  uint32_t tile_far = 1;
+  // far position; one-state ops were slower tiled on 2^10 / 2^11-chunk tiles (apply 77 -> 68 %
+  // at some positions), but on 2^12-chunk tiles (tile1_wide = 2) they lift the positions the
+  // direct rows lose (apply_q1 at 20 / 24 69.9 / 69.2 -> 71.6 / 71.5 %, apply_q2 (5,20) 68.0 ->
+  // 70.8 %, profiles/r4k_micro_tune.log): bits 0 and 1 on
+  uint32_t tile_far = 3;
   // XCD-aware block order of streaming single-gate launches (direct and tile families; knob
   // QDC_XCD_MAP): the blocks one XCD runs own adjacent ranges.  Measured at n = 28
   // (profiles/r2t_micro_table_xcd*.txt): injections at q1 1..6 71 -> 76 %, apply/inject at
@@ -140,10 +142,12 @@ struct Ctx {
   // of 2^9 (knob QDC_TILE2_WIDE): longer rows per far row bit.  Measured at n = 28
   // (profiles/r2y_micro_table_tile2_wide*.txt): reverse_q2 +1.2..3.3 points on every pair
   // ((26,27) 66.3 -> 69.6 %, (14,13) 69.4 -> 71.4 %), reverse_q1 and injections within +-0.5
-  uint32_t tile2_wide = 1;
-  // one-state tile-family launches on 2^11-chunk tiles (K = 8, 32 KiB of LDS) instead of 2^10
-  // (knob QDC_TILE1_WIDE)
-  uint32_t tile1_wide = 0;
+  // (round 4: 2^11-chunk two-state tiles, 64 KiB of LDS: reverse_q2 (26,27) 69.4 -> 72.3 %,
+  // (14,13) 71.3 -> 73.8 %, reverse_q1 75.8 -> 77.5-78 %, profiles/r4k_micro_tune.log)
+  uint32_t tile2_wide = 2;
+  // one-state tile-family launches on 2^(10 + tile1_wide)-chunk tiles (1: K = 8, 32 KiB of LDS;
+  // 2: K = 16, 64 KiB; knob QDC_TILE1_WIDE)
+  uint32_t tile1_wide = 2;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
