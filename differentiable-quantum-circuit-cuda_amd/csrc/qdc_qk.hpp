@@ -242,7 +242,10 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   // 16-B accesses (two adjacent groups per lane) when qubit 0 is not a target (f32); measured
   // at n = 28 (tools/qk_probe.py): k = 3 +5-7 %, k = 5 +5 %, k = 4 -10 % (kept at 8 B)
   bool pair = sizeof(real) == 4 && g.sorted[0] != 0 && k != 4;
-  if (const char* ev = getenv("QDC_QK_PAIR")) pair = pair && atoi(ev) != 0;
+  if (const char* ev = getenv("QDC_QK_PAIR")) {
+    const int v = atoi(ev);  // 0 off, 2: also at k = 4 (A/B)
+    pair = v == 2 ? sizeof(real) == 4 && g.sorted[0] != 0 : pair && v != 0;
+  }
   // batches per wave iteration (k_qk NB): 4 / 2 / 1 at k = 3 / 4 / 5, doubled ("wide": more
   // bytes in flight per wave) at k >= 4 — measured at n = 28 (tools/qk_probe.py,
   // profiles/r2o_qk_probe.log): k = 3 neutral, k = 4 +2 %, k = 5 +7 %.  Knob QDC_QK_WIDE=0/1
@@ -253,18 +256,23 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   // (tools/qk_probe.py --pf, profiles/r4i_qk_pf_ab.log): k = 3 0.643 -> 0.676, k = 5 0.515 ->
   // 0.562 of HBM, k = 4 0.573 -> 0.568; on by default at k = 3, 5
   const char* epf = getenv("QDC_QK_PF");
-  const bool pf = epf ? atoi(epf) != 0 : k != 4;
+  const int pfv = epf ? atoi(epf) : (k != 4 ? 1 : 0);
+  const bool pf = pfv != 0;
+  const bool pfwide = pfv == 2;  // pipelined with the doubled batches (A/B)
   if (pf) wide = false;
-  const uint64_t nb = (k == 3 ? 4 : k == 4 ? 2 : 1) * (wide ? 2 : 1);
+  const uint64_t nb = (k == 3 ? 4 : k == 4 ? 2 : 1) * ((wide || pfwide) ? 2 : 1);
   const uint64_t gpb = pair ? 32 : 16;  // groups per batch
   const uint64_t waves = ((g.ngroups + gpb - 1) / gpb + nb - 1) / nb;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 256u * 16u);
+  uint32_t gmax = 256u * 16u;  // blocks (QDC_QK_GRID: another cap, A/B)
+  if (const char* eg = getenv("QDC_QK_GRID")) gmax = (uint32_t)std::max(1, atoi(eg));
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3) / 4, gmax);
   c.next_flops = 8.0 * C * (double)((uint64_t)1 << n);  // C complex MACs per amplitude
   const double bytes = 2.0 * state_bytes(n);
   const real* buf = ring.dev[slot];
   const char* e;
 #define QDC_QK_LAUNCH(KK, PP, NB3)                                                              \
-  e = pf     ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3), true>, grid, 256u, s, buf, g) \
+  e = pfwide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3), true>, grid, 256u, s, buf, g) \
+      : pf   ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3), true>, grid, 256u, s, buf, g) \
       : wide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3)>, grid, 256u, s, buf, g)   \
              : c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3)>, grid, 256u, s, buf, g)
 #ifndef QDC_F64

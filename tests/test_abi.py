@@ -88,6 +88,19 @@ def test_flatten_helpers():
         _array1(np.zeros((2, 2), np.complex64), np.dtype(np.complex64), "x")
     with pytest.raises(q.PanicException, match="Gate is not contiguous."):
         _flatten([np.zeros(8, np.complex64)[::2]], np.complex64, "x", "Gate is not contiguous.")
+    # the one-pass gate path: same result, same errors as _array1 + _flatten
+    from quantum_differentiable_circuit import _flat_gates
+    dt = np.dtype(np.complex64)
+    flat2, lens2 = _flat_gates(g, dt, "x")
+    assert np.array_equal(flat2, flat) and list(lens2) == [4, 16] and lens2.dtype == np.uintp
+    with pytest.raises(TypeError, match="argument 'var_gates'"):
+        _flat_gates(g + [np.zeros(4, np.complex128)], dt, "var_gates")
+    with pytest.raises(TypeError):
+        _flat_gates([[1, 2]], dt, "x")
+    with pytest.raises(q.PanicException, match="Gate is not contiguous."):
+        _flat_gates([np.zeros(8, np.complex64)[::2]], dt, "x")
+    empty, elens = _flat_gates([], dt, "x")
+    assert empty.size == 1 and elens.size == 1
 
 
 # ------------------------------------------------------------------------------------------
