@@ -254,9 +254,11 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   // software-pipelined batches (k_qk PF; knob QDC_QK_PF=0/1): NB batches in flight while the
   // previous NB run on the matrix cores — replaces "wide" (same registers).  Measured at n = 28
   // (tools/qk_probe.py --pf, profiles/r4i_qk_pf_ab.log): k = 3 0.643 -> 0.676, k = 5 0.515 ->
-  // 0.562 of HBM, k = 4 0.573 -> 0.568; on by default at k = 3, 5
+  // 0.562 of HBM, k = 4 0.573 -> 0.568; on by default at k = 3, 5.  With the doubled batches
+  // (QDC_QK_PF=2, profiles/r4m_qk_ab.log): k = 3 0.676 -> 0.705, k = 4 0.577 -> 0.580, k = 5
+  // 0.563 -> 0.549: the default at k = 3
   const char* epf = getenv("QDC_QK_PF");
-  const int pfv = epf ? atoi(epf) : (k != 4 ? 1 : 0);
+  const int pfv = epf ? atoi(epf) : (k == 3 ? 2 : k == 5 ? 1 : 0);
   const bool pf = pfv != 0;
   const bool pfwide = pfv == 2;  // pipelined with the doubled batches (A/B)
   if (pf) wide = false;
