@@ -51,6 +51,10 @@ def bench_name(kernel):
         return "zero"
     if "k_finalize" in kernel:
         return "finalize"
+    if "k_diag_inject" in kernel:
+        return "inject_diag"
+    if "k_dsum" in kernel:
+        return "dsum"
     return None
 
 
