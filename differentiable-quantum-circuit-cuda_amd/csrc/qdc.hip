@@ -519,12 +519,15 @@ static const char* spec_program_for(unsigned tile_bits, const unsigned* kinds, c
   // tile_bits | 0x100: a one-state pass on the two-state tile size (f32: one wave, five slots)
   // | 0x200 as well: that pass prefetching the next tile (f32 one-wave: k_rw<false, 2, true, 1, true>)
   const bool force_one = (tile_bits & 0x100u) != 0, pf = (tile_bits & 0x200u) != 0;
+  const unsigned tile_bits_in = tile_bits;
   tile_bits &= 0xffu;
   const unsigned t2bits = sizeof(qdc::real) == 4 ? 11u : 10u;
   if (tile_bits != t2bits && tile_bits != t2bits + 1) return "tile_bits: not a specialized pass's tile";
   const bool two = tile_bits == t2bits && !force_one;
   const qdc::SpecKind K = two ? qdc::spec_kind_two() : qdc::spec_kind_one(tile_bits, pf);
-  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, K.ns);
+  const bool keep = K.ns == 5 && tile_bits == 11 && !pf && !(tile_bits_in & 0x400u) &&
+                    sizeof(qdc::real) == 4;  // (as the runtime's spec_half planning)
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, true, K.ns, keep);
   std::vector<qdc::SpecStep> sst;
   qdc::RqLayout cur = plan.load;
   for (const qdc::RqStep& s : plan.steps) {
@@ -542,9 +545,13 @@ static const char* spec_program_for(unsigned tile_bits, const unsigned* kinds, c
       F.t1 = (s.cs & 7u) * 8u + (s.cs >> 3);  // the runtime's canonical S1 < S2
     sst.push_back(qdc::SpecStep{false, cur, cur, F});
   }
-  const std::string body = qdc::spec_program_source(sst, tile_bits, K);
-  name = qdc::spec_kernel_name(body, K);
-  src = qdc::spec_kernel_source(name, body, K);
+  // (the runtime's choice: a one-wave one-state program whose relayouts all keep a slot runs on
+  // half buffers, qdc_circuit.hpp half1; | 0x400 keeps the full buffer)
+  const bool half = keep && qdc::spec_half_ok(sst);
+  const qdc::SpecKind KK = !half ? K : two ? qdc::spec_kind_two(true) : qdc::spec_kind_one(tile_bits, false, true);
+  const std::string body = qdc::spec_program_source(sst, tile_bits, KK);
+  name = qdc::spec_kernel_name(body, KK);
+  src = qdc::spec_kernel_source(name, body, KK);
   return nullptr;
 }
 
@@ -626,7 +633,9 @@ QDC_API size_t qdc_rq_plan(unsigned tile_bits, unsigned slots, const unsigned* k
   std::vector<qdc::RqStage> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = qdc::RqStage{kinds[i], t1[i], t2[i], deps ? deps[i] : 0};
   const char* mc = getenv("QDC_RQ_MAXCL");  // the runtime's knob (qdc_circuit.hpp)
-  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, !(mc && atoi(mc) == 0), slots);
+  const char* kp = getenv("QDC_RQ_KEEP");  // (tests: the half-buffer planning, rq_plan keep)
+  const qdc::RqPlan plan = qdc::rq_plan(st, tile_bits, nullptr, !(mc && atoi(mc) == 0), slots,
+                                        kp && atoi(kp) != 0);
   if (plan.steps.size() + 2 > cap) return SIZE_MAX;
   auto put = [&](size_t i, unsigned kind, unsigned stage, unsigned cs, const qdc::RqLayout& L) {
     unsigned* o = steps + 8 * i;

@@ -287,6 +287,9 @@ struct Circuit {
   // schedules itself as usual).  On by default (round 4: C5 n = 14 f32 uncompute 4.85x -> 1.4x
   // the reference's floor; C2 n = 28 f32 ~3.5 % slower, DESIGN.md "Uncompute drift").
   int mirror = 1;
+  // one-state one-wave specialized passes relayout through half the LDS buffer when every
+  // relayout keeps a register slot (QDC_SPEC_HALF; twice the resident waves)
+  int spec_half = 1;
   // trailing one-qubit stages of a pass join their qubit's next two-qubit stage in a later pass
   // (qdc_fusion.hpp defer_trailing_q1; QDC_DEFER_Q1)
   int defer_q1 = 1;
@@ -361,6 +364,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
     if (const char* e = getenv("QDC_MIRROR")) mirror = atoi(e);
+    if (const char* e = getenv("QDC_SPEC_HALF")) spec_half = atoi(e);
     if (const char* e = getenv("QDC_DEFER_Q1")) defer_q1 = atoi(e);
     if (const char* e = getenv("QDC_SCHED_CACHE")) sched_cache_on = atoi(e);
     if (const char* e = getenv("QDC_TILE1_CHUNKS")) {
@@ -859,8 +863,8 @@ struct Circuit {
   // register-layout plans of passes (rq_plan, ~20 us each), by the pass's stages and tile
   std::map<std::vector<uint64_t>, RqPlan> rq_plan_cache;
   const RqPlan& rq_plan_cached(const std::vector<RqStage>& rs, uint32_t tbits, const uint32_t* src,
-                               bool maxcl, uint32_t ns) {
-    std::vector<uint64_t> key = {tbits, ns, maxcl ? 1u : 0u, src ? 1u : 0u};
+                               bool maxcl, uint32_t ns, bool keep = false) {
+    std::vector<uint64_t> key = {tbits, ns, (maxcl ? 1u : 0u) | (keep ? 2u : 0u), src ? 1u : 0u};
     if (src)
       for (int i = 0; i < 4; ++i) key.push_back(src[i]);
     for (const RqStage& r : rs) {
@@ -870,7 +874,7 @@ struct Circuit {
     auto it = rq_plan_cache.find(key);
     if (it != rq_plan_cache.end()) return it->second;
     if (rq_plan_cache.size() >= 8192) rq_plan_cache.clear();
-    return rq_plan_cache.emplace(std::move(key), rq_plan(rs, tbits, src, maxcl, ns)).first->second;
+    return rq_plan_cache.emplace(std::move(key), rq_plan(rs, tbits, src, maxcl, ns, keep)).first->second;
   }
   std::vector<std::vector<uint32_t>> stage_partition(const std::vector<uint32_t>& pass,
                                                      const std::vector<qdc_plan_op>& plan,
@@ -1223,7 +1227,8 @@ struct Circuit {
                                    (rq_fwd5 && it.tbits == 12));  // k_rw W = 2, prefetching
       const uint32_t ns = (sizeof(real) == 4 && (s5_two || s5_one)) ? 5u : 4u;
       it.s5 = ns == 5;
-      const RqPlan& P = rq_plan_cached(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns);
+      const bool keep = spec_half && ns == 5 && it.tbits == 11 && sizeof(real) == 4;
+      const RqPlan& P = rq_plan_cached(rs, it.tbits, perm ? src : nullptr, rq_maxcl != 0, ns, keep);
       it.l0 = put_layout(P.load);
       {  // rqio after the load descriptor
         rqio io{};
@@ -1293,7 +1298,10 @@ struct Circuit {
         // the source is generated once per distinct program (per process): the key is
         // everything it depends on, the layouts, stage kinds, slot cases and Γ flags
         const bool pf1 = spec1 && it.s5 && rw1_prefetch();
-        std::vector<uint32_t> key = {spec1 ? 1u : 2u, it.tbits, spec_imm() ? 1u : 0u, pf1 ? 1u : 0u};
+        const bool half1 = it.s5 && it.tbits == 11 && !pf1 && spec_half && !spec_imm() &&
+                           sizeof(real) == 4 && spec_half_ok(sst);
+        std::vector<uint32_t> key = {spec1 ? 1u : 2u, it.tbits, spec_imm() ? 1u : 0u,
+                                     (pf1 ? 1u : 0u) | (half1 ? 2u : 0u)};
         auto put_layout_key = [&](const RqLayout& L) {
           key.push_back(L.ns | (L.tfix ? 0x100u : 0u));
           for (uint32_t q = 0; q < RQ_SLOTS_MAX; ++q) key.push_back(L.slot[q]);
@@ -1311,7 +1319,7 @@ struct Circuit {
         }
         auto hit = spec_cache.find(key);
         if (hit == spec_cache.end()) {
-          const SpecKind K = spec1 ? spec_kind_one(it.tbits, pf1) : spec_kind_two();
+          const SpecKind K = spec1 ? spec_kind_one(it.tbits, pf1, half1) : spec_kind_two(half1);
           const std::string body = spec_program_source(sst, it.tbits, K);
           SpecEntry e;
           e.name = spec_kernel_name(body, K);
@@ -1492,6 +1500,7 @@ struct Circuit {
                                        : (const void*)k_rw<false, 2, false, 2>;
       uint32_t grid = 0;
       QDC_TRY(fused_grid(fg, kw, (int)bs, grid));
+      if (nt == 128 && s5 && spec && !(two && pfw)) QDC_TRY(fused_grid_fn(spec, (int)bs, grid));
       fgeo g = fg;
       // one wave per block: static shares + a dynamic tail
       if (!(bs == 64 && !pfw && grid >= 8 && g.ntiles >= 4ull * grid && ctx.plan_dyn(g, grid))) {
@@ -1601,6 +1610,26 @@ struct Circuit {
 #endif
   }
   // one wave of resident blocks (occupancy query, cached per kernel), or QDC_FUSED_BLOCKS
+  // (a specialized kernel: its own occupancy, which may differ from the interpreted one's)
+  const char* fused_grid_fn(hipFunction_t fn, int nt, uint32_t& grid) {
+    if (fused_blocks) {
+      grid = fused_blocks;
+      return nullptr;
+    }
+    const void* key = (const void*)fn;
+    for (auto& e : fused_resident_cache)
+      if (e.first == key) {
+        grid = e.second;
+        return nullptr;
+      }
+    int per_cu = 0, dev = 0, cus = 0;
+    QDC_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0));
+    QDC_HIP(hipGetDevice(&dev));
+    QDC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    grid = (uint32_t)std::max(1, std::min(per_cu * cus, (int)NBMAX));
+    fused_resident_cache.push_back({key, grid});
+    return nullptr;
+  }
   const char* fused_grid(const fgeo& fg, const void* kernel, int nt, uint32_t& grid) {
     if (fused_blocks) {
       grid = fused_blocks;

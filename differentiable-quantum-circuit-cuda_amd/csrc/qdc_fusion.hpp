@@ -577,8 +577,11 @@ inline void rq_hbm(const RqLayout& L, uint32_t T, uint32_t lc, const uint32_t* h
 // layout chosen the same way under the HBM constraint, and ends in an HBM-valid layout — for
 // a permuting pass (src != nullptr: src[b] = the tile bit whose value lands on tile bit b,
 // b < 4) the layout with slot 0 = src[0] and thread bits 0..2 = src[1..3].
+// keep: every relayout keeps one register slot's tile bit in place (a cover includes a qubit of
+// the current slots), so it can run through half the LDS buffer (qdc_spec.hpp spec_xchg_half)
 inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
-                      const uint32_t* src = nullptr, bool max_closure = true, uint32_t ns = 4) {
+                      const uint32_t* src = nullptr, bool max_closure = true, uint32_t ns = 4,
+                      bool keep = false) {
   const size_t n = st.size();
   auto qset = [&](size_t j, uint32_t* q) -> int {
     q[0] = st[j].t1;
@@ -710,7 +713,29 @@ inline RqPlan rq_plan(const std::vector<RqStage>& st, uint32_t T,
         S = best_cover(done, LV == 1 ? std::vector<uint32_t>{0u} : std::vector<uint32_t>{}, true);
         hbm = closure(done, S) == (int)left;
       }
-      if (!hbm) S = best_cover(done, {}, false);
+      if (hbm && keep) {  // the HBM cover must keep one of the current slots in place
+        const RqLayout L = place(S, cur, true);
+        bool kept = false;
+        for (uint32_t q = 0; q < ns; ++q) kept = kept || (L.slot[q] == cur.slot[q] && cur.slot[q] != ~0u);
+        hbm = kept;
+      }
+      if (!hbm && keep) {  // the best cover that contains one of the current slots' qubits
+        // (f32: tile bit 0 stays in slot 0 when it is there, so the HBM store layout, which
+        // needs it there, keeps that slot too)
+        int best_cnt = -1;
+        const bool pin0 = LV == 1 && cur.slot[0] == 0;
+        for (uint32_t q = 0; q < ns; ++q) {
+          if (cur.slot[q] == ~0u || (pin0 && q != 0)) continue;
+          std::vector<uint32_t> Sq = best_cover(done, {cur.slot[q]}, false);
+          const int cnt = closure(done, Sq);
+          if (cnt > best_cnt) {
+            best_cnt = cnt;
+            S = std::move(Sq);
+          }
+        }
+      } else if (!hbm) {
+        S = best_cover(done, {}, false);
+      }
       cur = place(S, cur, hbm);
       P.steps.push_back(RqStep{true, cur, 0, 0});
       for (size_t j = 0; j < n && pick == n; ++j)

@@ -78,17 +78,24 @@ struct SpecKind {
   const char* pass;    // the generic kernel's body with the program
   uint32_t threads;
   const char* waves;   // amdgpu_waves_per_eu of the generic kernel
+  bool half = false;   // relayouts through half the buffer (spec_xchg_half)
 };
 #ifndef QDC_F64
 // k_rw<true, 2, false, 1, true>: f32 two-state, one wave, five slots
-inline SpecKind spec_kind_two() {
+inline SpecKind spec_kind_two(bool half = false) {
+  if (half)  // every relayout in two rounds through half the buffer
+    return {true, 6, 5, false, "qdc_spec_", "qdc::rw_pass<true, 2, false, 1, true, Prog, true>", 64,
+            "QDC_RW_WAVES, QDC_RW_WAVES", true};
   return {true, 6, 5, false, "qdc_spec_", "qdc::rw_pass<true, 2, false, 1, true, Prog>", 64,
           "QDC_RW_WAVES, QDC_RW_WAVES"};
 }
 // k_rq<false, 256, true>: f32 one-state 2^12 tiles, four waves, prefetching; k_rw<false, 2,
 // false, 1, true>: 2^11 tiles (QDC_TILE1_CHUNKS=1024, QDC_RW bit 1), one wave, five slots
 // (pf: the next tile prefetched into pinned VGPRs, k_rw<false, 2, true, 1, true>, QDC_RW bit 3)
-inline SpecKind spec_kind_one(uint32_t T, bool pf = false) {
+inline SpecKind spec_kind_one(uint32_t T, bool pf = false, bool half = false) {
+  if (T == 11 && half && !pf)  // every relayout in two rounds through half the buffer
+    return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, false, 1, true, Prog, true>", 64,
+            "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE", true};
   if (T == 11 && pf)
     return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, true, 1, true, Prog>", 64,
             "QDC_RW_WAVES, QDC_RW_WAVES"};
@@ -100,12 +107,12 @@ inline SpecKind spec_kind_one(uint32_t T, bool pf = false) {
 }
 #else
 // k_rw<true, 1, false, 1>: f64 two-state, one wave
-inline SpecKind spec_kind_two() {
+inline SpecKind spec_kind_two(bool = false) {
   return {true, 6, 4, false, "qdc_spec_d_", "qdc::rw_pass<true, 1, false, 1, false, Prog>", 64,
           "QDC_RW_WAVES, QDC_RW_WAVES"};
 }
 // k_rw<false, 1, false, W>: f64 one-state, W = 1 (2^10 tiles) or 2 (2^11)
-inline SpecKind spec_kind_one(uint32_t T, bool = false) {
+inline SpecKind spec_kind_one(uint32_t T, bool = false, bool = false) {
   if (T == 10)
     return {false, 6, 4, false, "qdc_specf_d_", "qdc::rw_pass<false, 1, false, 1, false, Prog>", 64,
             "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};
@@ -113,6 +120,39 @@ inline SpecKind spec_kind_one(uint32_t T, bool = false) {
           "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE"};
 }
 #endif
+// The register slot a relayout keeps (the same tile bit in the same slot of both layouts), or
+// -1: a half-buffer relayout splits on it (spec_xchg_half).
+inline int spec_kept_slot(const RqLayout& Lc, const RqLayout& Ln) {
+  if (Lc.ns != Ln.ns) return -1;
+  for (uint32_t s = 0; s < Lc.ns; ++s)
+    if (Lc.slot[s] == Ln.slot[s] && Lc.slot[s] != ~0u) return (int)s;
+  return -1;
+}
+// A one-state one-wave program whose every relayout keeps a slot runs on half buffers.
+inline bool spec_half_ok(const std::vector<SpecStep>& steps) {
+  bool any = false;
+  for (const SpecStep& s : steps)
+    if (s.relayout) {
+      any = true;
+      if (spec_kept_slot(s.Lc, s.Ln) < 0) return false;
+    }
+  return any;
+}
+// the layout's LDS descriptor on the index without tile bit b (rq_descriptor, compressed)
+inline rq_layout rq_descriptor_without(const RqLayout& L, uint32_t T, uint32_t b) {
+  auto cut = [&](uint32_t i) { return (i & ((1u << b) - 1u)) | ((i >> (b + 1)) << b); };
+  rq_layout d{};
+  for (uint32_t j = 0; j < (1u << L.ns); ++j) {
+    uint32_t idx = 0;
+    for (uint32_t s = 0; s < L.ns; ++s)
+      if ((j >> s) & 1u) idx |= 1u << L.slot[s];
+    d.rp[j] = swz(cut(idx));
+  }
+  uint32_t th[8];
+  const uint32_t nt = L.threads(T, th);
+  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = swz(cut(1u << th[k]));
+  return d;
+}
 inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint32_t T, const SpecKind& K) {
   std::string b;
   char tmp[512];
@@ -158,6 +198,17 @@ inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint3
            "] = " + arr(offr, NR) + ";\n      ";
       b += K.two ? "spec_xchg_imm" + xt + "(xf, E, pn, offr); spec_xchg_imm" + xt + "(xb, E, pn, offr); }\n"
                  : "spec_xchg_imm" + xt + "(x, E, pn, offr); }\n";
+      continue;
+    }
+    if (s.relayout && K.half) {
+      const int ks = spec_kept_slot(s.Lc, s.Ln);
+      const uint32_t bit = s.Lc.slot[ks];
+      const rq_layout c = rq_descriptor_without(s.Lc, T, bit), n = rq_descriptor_without(s.Ln, T, bit);
+      b += "    { constexpr uint32_t rc[" + nr + "] = " + arr(c.rp, NR) + ", tc[8] = " + arr(c.tv, 8) +
+           ", rn[" + nr + "] = " + arr(n.rp, NR) + ", tn[8] = " + arr(n.tv, 8) + ";\n      ";
+      const std::string xh = "spec_xchg_half<" + std::to_string(TB) + ", " + nr + ", " + std::to_string(ks) + ">";
+      b += K.two ? xh + "(xf, E, rc, tc, rn, tn); " + xh + "(xb, E, rc, tc, rn, tn); }\n"
+                 : xh + "(x, E, rc, tc, rn, tn); }\n";
       continue;
     }
     if (s.relayout) {

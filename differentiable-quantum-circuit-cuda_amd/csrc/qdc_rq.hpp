@@ -724,7 +724,7 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 // k_rq (rq_ld / rq_vmwait_two), with a dynamic tail taken block-wide.
 // PROG (not void; non-prefetching instances): the pass program as straight-line stage calls
 // (qdc_spec.hpp) in place of the interpreted op loop.
-template <bool TWO, int NE, bool PF, int W, bool S5 = false, class PROG = void>
+template <bool TWO, int NE, bool PF, int W, bool S5 = false, class PROG = void, bool HALF = false>
 __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict__ b,
                                         const fop* __restrict__ ops, const cx* __restrict__ mats,
                                         fgeo fg, uint32_t l0, cx* __restrict__ partials,
@@ -738,7 +738,10 @@ __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict
   constexpr int R = RQ_R * NE;   // amplitudes per lane and state
   constexpr int CPT = R / VEC;   // chunks per lane and state
   constexpr int CPG = RQ_R / VEC;  // chunks per register group (f32 8, f64 16)
-  __shared__ cx buf[64 * W * R];
+  // (HALF: a specialized one-wave program whose every relayout runs in two rounds through half
+  // the buffer, qdc_spec.hpp spec_xchg_half)
+  static_assert(!HALF || (W == 1 && !std::is_void<PROG>::value), "half buffers: one-wave programs");
+  __shared__ cx buf[64 * W * R / (HALF ? 2 : 1)];
   __shared__ real accw[TWO ? FMAX_GRAD_RQ : 1][FACC];
   const uint32_t lane = threadIdx.x;  // the block's thread (W = 1: the lane)
   if constexpr (TWO) {

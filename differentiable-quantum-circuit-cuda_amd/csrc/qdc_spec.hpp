@@ -52,6 +52,40 @@ __device__ __forceinline__ void spec_xchg(cx (&x)[R], const SpecEnv& E, const ui
   if constexpr (!BAR) __builtin_amdgcn_wave_barrier();
 }
 
+// One-wave exchange through half the buffer: a tile bit that both layouts hold in the same
+// register slot S splits it into two rounds, each moving the registers with slot bit S = p
+// through an LDS index without that bit (rpc / rpn / tvc / tvn are formed on the compressed
+// index, qdc_jit.hpp).  A round writes and reads the same registers, so nothing is overwritten
+// before it is written; the kernel then needs 2^(T-1) * 8 B of LDS per wave instead of 2^T * 8
+// (one-state five-slot tiles: 8 KiB, so LDS no longer caps them at 2.5 waves per SIMD).
+template <int TB, int R, int S>
+__device__ __forceinline__ void spec_xchg_half(cx (&x)[R], const SpecEnv& E, const uint32_t* rpc,
+                                               const uint32_t* tvc, const uint32_t* rpn,
+                                               const uint32_t* tvn) {
+  uint32_t tp = 0, tpn = 0;
+#pragma unroll
+  for (int k = 0; k < TB; ++k) {
+    tp ^= ((E.t >> k) & 1u) ? tvc[k] : 0u;
+    tpn ^= ((E.t >> k) & 1u) ? tvn[k] : 0u;
+  }
+  uint32_t tpb = tp * (uint32_t)sizeof(cx), tpnb = tpn * (uint32_t)sizeof(cx);
+  asm volatile("" : "+v"(tpb), "+v"(tpnb));
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (((j >> S) & 1) == p)
+        *reinterpret_cast<cx*>(__builtin_assume_aligned(E.bufb + (tpb ^ (rpc[j] * (uint32_t)sizeof(cx))), 8)) = x[j];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (((j >> S) & 1) == p)
+        x[j] = *reinterpret_cast<const cx*>(
+            __builtin_assume_aligned(E.bufb + (tpnb ^ (rpn[j] * (uint32_t)sizeof(cx))), 8));
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // The same exchange with LDS addresses that need no VALU per access: the LDS index is a bit
 // permutation of the tile index that puts the current layout's thread bits on index bits
 // 0..TB-1 and its register slots above, so every write goes to t * sizeof(cx) + j * 2^TB *

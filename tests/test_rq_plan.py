@@ -97,3 +97,28 @@ def test_rq_plan_five_slots_fewer_relayouts(brick):
                                     "f32", sl)
     print("relayouts 4 / 5 slots:", total)
     assert total[5] < total[4], total
+
+
+@pytest.mark.parametrize("brick", [False, True])
+def test_rq_plan_keep_slot_for_half_buffers(monkeypatch, brick):
+    """rq_plan keep (QDC_RQ_KEEP; the runtime's one-wave five-slot passes): every relayout keeps
+    one register slot's tile bit in the same slot, so the exchange runs in two rounds through
+    half the LDS buffer (qdc_spec.hpp spec_xchg_half).  Plans stay valid; the cost in relayouts
+    over a set of passes is printed and bounded."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(31 + brick)
+    total = {"0": 0, "1": 0}
+    for _ in range(120):
+        stages, deps = random_pass(rng, 11, int(rng.integers(4, 40)), brick)
+        for keep in ("0", "1"):
+            monkeypatch.setenv("QDC_RQ_KEEP", keep)
+            plan = q.rq_plan(11, stages, deps, precision="f32", slots=5)
+            total[keep] += check_plan(11, stages, deps, plan, "f32", 5)
+            if keep == "1":
+                cur = list(plan[0])
+                for s in plan[1]:
+                    if s["relayout"]:
+                        assert any(a == b for a, b in zip(cur, s["slots"])), (cur, s["slots"])
+                        cur = list(s["slots"])
+    print("relayouts without / with a kept slot:", total)
+    assert total["1"] <= 1.5 * total["0"], total

@@ -352,3 +352,32 @@ def test_spec_one_wave_forward_pass_kernel(tmp_path, pf):
     meta = text[text.index(".amdhsa_kernel " + name):]
     assert int(meta.split(".amdhsa_next_free_vgpr")[1].split()[0]) <= 256
     assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
+
+
+@pytest.mark.parametrize("tile_bits,prefix", [(11 | 0x100, "qdc_specf_"), (11, "qdc_spec_")])
+def test_spec_half_buffer_relayouts(tmp_path, tile_bits, prefix):
+    """One-wave five-slot programs (one-state 2^11 tiles and the two-state reverse passes) plan
+    every relayout to keep a register slot in place (rq_plan keep) and exchange through half the
+    LDS buffer in two rounds (spec_xchg_half): 8 KiB (one-state) / 10 KiB (two-state, with the
+    Gamma accumulators) of LDS per wave instead of 16 / 18, no scratch.  | 0x400 keeps the full
+    buffer (another kernel)."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(23)
+    stages, deps = random_pass(rng, 11, 14, brick=True)
+    name, obj = q.spec_selftest(tile_bits, stages, deps)
+    full, _ = q.spec_selftest(tile_bits | 0x400, stages, deps)
+    assert name.startswith(prefix) and full.startswith(prefix) and name != full
+    src = os.path.join(os.path.dirname(obj), name + "." + str(os.getpid()) + ".hip")
+    assert "spec_xchg_half<" in open(src).read() and "Prog, true>" in open(src).read()
+    csrc = os.path.join(os.path.dirname(q.__file__), "..", "csrc")
+    inc = os.path.join(csrc, "..", "..", "include")
+    asm = tmp_path / "k.s"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "-I" + inc, "-I" + csrc, "-S", "--cuda-device-only", "-o", str(asm), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = asm.read_text()
+    meta = text[text.index(".amdhsa_kernel " + name):]
+    lds = int(meta.split(".amdhsa_group_segment_fixed_size")[1].split()[0])
+    assert lds == (8192 if tile_bits & 0x100 else 10240), lds
+    assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
