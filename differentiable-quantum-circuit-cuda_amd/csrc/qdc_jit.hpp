@@ -93,9 +93,12 @@ inline SpecKind spec_kind_two(bool half = false) {
 // false, 1, true>: 2^11 tiles (QDC_TILE1_CHUNKS=1024, QDC_RW bit 1), one wave, five slots
 // (pf: the next tile prefetched into pinned VGPRs, k_rw<false, 2, true, 1, true>, QDC_RW bit 3)
 inline SpecKind spec_kind_one(uint32_t T, bool pf = false, bool half = false) {
-  if (T == 11 && half && !pf)  // every relayout in two rounds through half the buffer
+  // every relayout in two rounds through half the buffer (8 KiB of LDS per wave): compiled for
+  // QDC_RW_WAVES_HALF_ONE [5] waves per SIMD, which LDS now allows (~96 VGPRs, a few spilled;
+  // 4 waves at 106 VGPRs measured 0.7-1.0 % slower per step, profiles/r4s)
+  if (T == 11 && half && !pf)
     return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, false, 1, true, Prog, true>", 64,
-            "QDC_RW_WAVES_ONE, QDC_RW_WAVES_ONE", true};
+            "QDC_RW_WAVES_HALF_ONE, QDC_RW_WAVES_HALF_ONE", true};
   if (T == 11 && pf)
     return {false, 6, 5, false, "qdc_specf_", "qdc::rw_pass<false, 2, true, 1, true, Prog>", 64,
             "QDC_RW_WAVES, QDC_RW_WAVES"};
@@ -323,15 +326,19 @@ inline bool spec_source_fp(const std::string& csrc, const std::string& inc, uint
 #ifndef QDC_NT_STORE
 #define QDC_NT_STORE 1
 #endif
+#ifndef QDC_RW_WAVES_HALF_ONE
+#define QDC_RW_WAVES_HALF_ONE 5
+#endif
 inline std::string spec_defines() {
   char b[512];
   snprintf(b, sizeof b,
            "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
            "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d "
-           "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d%s",
+           "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d -DQDC_RW_WAVES_HALF_ONE=%d%s",
            (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
            (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, sizeof(real) == 8 ? " -DQDC_F64" : "");
+           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE,
+           sizeof(real) == 8 ? " -DQDC_F64" : "");
   return b;
 }
 // hipcc options of every specialized kernel besides the defines and include paths

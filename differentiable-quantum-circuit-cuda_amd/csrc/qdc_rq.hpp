@@ -711,6 +711,9 @@ void k_rq(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict__ 
 #endif
 // one-state passes without prefetch (the f64 forward by default): 16 amplitudes per lane in f64
 // need ~135 VGPRs, which 2 waves/SIMD would leave half idle
+#ifndef QDC_RW_WAVES_HALF_ONE  // specialized one-state half-buffer passes (qdc_jit.hpp)
+#define QDC_RW_WAVES_HALF_ONE 5
+#endif
 #ifndef QDC_RW_WAVES_ONE
 #define QDC_RW_WAVES_ONE 2
 #endif

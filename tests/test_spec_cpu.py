@@ -338,7 +338,7 @@ def test_spec_one_wave_forward_pass_kernel(tmp_path, pf):
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(21)
     stages, deps = random_pass(rng, 11, 12, brick=True)
-    name, obj = q.spec_selftest(11 | 0x100 | pf, stages, deps)
+    name, obj = q.spec_selftest(11 | 0x100 | 0x400 | pf, stages, deps)  # (full buffer)
     assert name.startswith("qdc_specf_") and os.path.getsize(obj) > 10000
     src = os.path.join(os.path.dirname(obj), name + "." + str(os.getpid()) + ".hip")
     csrc = os.path.join(os.path.dirname(q.__file__), "..", "csrc")
@@ -359,8 +359,8 @@ def test_spec_half_buffer_relayouts(tmp_path, tile_bits, prefix):
     """One-wave five-slot programs (one-state 2^11 tiles and the two-state reverse passes) plan
     every relayout to keep a register slot in place (rq_plan keep) and exchange through half the
     LDS buffer in two rounds (spec_xchg_half): 8 KiB (one-state) / 10 KiB (two-state, with the
-    Gamma accumulators) of LDS per wave instead of 16 / 18, no scratch.  | 0x400 keeps the full
-    buffer (another kernel)."""
+    Gamma accumulators) of LDS per wave instead of 16 / 18.  | 0x400 keeps the full buffer
+    (another kernel)."""
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(23)
     stages, deps = random_pass(rng, 11, 14, brick=True)
@@ -380,4 +380,11 @@ def test_spec_half_buffer_relayouts(tmp_path, tile_bits, prefix):
     meta = text[text.index(".amdhsa_kernel " + name):]
     lds = int(meta.split(".amdhsa_group_segment_fixed_size")[1].split()[0])
     assert lds == (8192 if tile_bits & 0x100 else 10240), lds
-    assert int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0]) == 0
+    # the one-state kind is compiled for 5 waves per SIMD (<= 102 VGPRs): a few registers of
+    # the relayout addressing spill (~50 B per lane, measured faster than 4 waves without)
+    scratch = int(meta.split(".amdhsa_private_segment_fixed_size")[1].split()[0])
+    vgpr = int(meta.split(".amdhsa_next_free_vgpr")[1].split()[0])
+    if tile_bits & 0x100:
+        assert scratch <= 128 and vgpr <= 102, (scratch, vgpr)
+    else:
+        assert scratch == 0, scratch
