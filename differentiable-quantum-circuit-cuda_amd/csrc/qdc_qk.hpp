@@ -174,6 +174,163 @@ __global__ __launch_bounds__(256) void k_qk(cx* __restrict__ s, const real* __re
   }
 }
 
+// LDS-staged tiles (k_qkl), for gates with low target qubits.  k_qk's lanes j of a quad own 16
+// consecutive groups, which are 16 consecutive chunks only when the low address bits are not
+// targets: with targets among them every load instruction touches 64 lines for 16 B each
+// (n = 28 f32, targets 1..5: 0.45 of HBM against 0.65 at 10..14, tools/qk_pos_probe.py).  Here a
+// tile is 16 whole groups: the address bits below h (the four lowest non-target bits and the
+// targets between them) plus every combination of the targets above h — 2^(k-L) contiguous
+// chunks of 2^h amplitudes (L = targets below h).  A wave loads a tile with 16-B lane-contiguous
+// accesses, stages it in LDS, each lane reads its MFMA operands (group j, amplitudes M q + m) and
+// writes the results back to the cells it read, and the tile leaves as it came.
+struct qkl_geo {
+  uint64_t choff[1 << QK_MAX];  // amplitude offset of chunk c (bit i of c: target hi[i])
+  uint32_t eoff[1 << QK_MAX];   // tile index of local amplitude ci in group 0
+  uint32_t eg[16];              // tile index of group j's amplitude 0
+  uint32_t hi[QK_MAX];          // targets >= h, ascending (tile base: insert zeros)
+  uint32_t nhi, h;
+  uint64_t ntiles;
+};
+
+// LDS cell of tile index e: XOR-swizzled within 256-B rows (16-B pieces stay whole), so the 16
+// groups a quad reads at one amplitude — spread by the target bits between them — spread over
+// the banks
+__device__ __forceinline__ uint32_t qkl_swz(uint32_t e) {
+  constexpr uint32_t PE = 256 / sizeof(cx);  // cells per 256-B row
+  return e ^ (((e / PE) % (PE / VEC)) * VEC);
+}
+
+template <int K, int NB>
+__global__ __launch_bounds__(256) void k_qkl(cx* __restrict__ s, const real* __restrict__ aop,
+                                             qkl_geo g) {
+  constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
+  constexpr int TA = 16 * C;          // amplitudes per tile
+  constexpr int NP = TA / VEC / 64;   // 16-B pieces per lane per tile
+  static_assert(NP >= 1, "tile smaller than one wave access");
+#ifdef QDC_F64
+  using acc_t = double __attribute__((ext_vector_type(4)));
+#else
+  using acc_t = float __attribute__((ext_vector_type(4)));
+#endif
+  __shared__ chunk lds[4][NB][TA / VEC];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = l >> 4, j = l & 15;
+  real a[T][S];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int u = 0; u < S; ++u) a[t][u] = aop[((size_t)t * S + u) * 64 + l];
+  uint32_t rd[M];  // this lane's operand cells
+#pragma unroll
+  for (int m = 0; m < M; ++m) rd[m] = qkl_swz(g.eoff[M * q + m] | g.eg[j]);
+  uint32_t pc[NP];  // this lane's pieces: LDS chunk and amplitude offset from the tile base
+  uint64_t po[NP];
+  const uint32_t hmask = (1u << g.h) - 1u;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const uint32_t e = (uint32_t)(i * 64 + l) * VEC;
+    pc[i] = qkl_swz(e) / VEC;
+    po[i] = g.choff[e >> g.h] + (e & hmask);
+  }
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  cx* cell = reinterpret_cast<cx*>(&lds[w][0][0]);
+  for (uint64_t t0 = wave * NB; t0 < g.ntiles; t0 += nwaves * NB) {
+    uint64_t base[NB];
+    chunk raw[NB][NP];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      base[nb] = (t0 + nb) << g.h;
+      for (uint32_t b = 0; b < g.nhi; ++b) base[nb] = insert_zero(base[nb], g.hi[b]);
+      if (t0 + nb < g.ntiles) {  // wave-uniform
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+          raw[nb][i] = ldc(reinterpret_cast<const chunk*>(s + base[nb] + po[i]));
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < NP; ++i) lds[w][nb][pc[i]] = raw[nb][i];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      cx x[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) x[m] = cell[nb * TA + rd[m]];
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        acc_t d = acc_t{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+          const real bv = (u & 1) ? x[u >> 1].y : x[u >> 1].x;
+#ifdef QDC_F64
+          d = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][u], bv, d, 0, 0, 0);
+#else
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u], bv, d, 0, 0, 0);
+#endif
+        }
+        // outputs: amplitudes M q + 2t and M q + 2t + 1 of group j (qk_operands' row order)
+        cell[nb * TA + rd[2 * t]] = cx{d[0], d[1]};
+        cell[nb * TA + rd[2 * t + 1]] = cx{d[2], d[3]};
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      if (t0 + nb < g.ntiles) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+          stc(reinterpret_cast<chunk*>(s + base[nb] + po[i]), lds[w][nb][pc[i]]);
+      }
+    __builtin_amdgcn_wave_barrier();  // the next tiles overwrite these cells
+  }
+}
+
+// k_qkl's geometry, or false when the state has fewer than four non-target qubits
+inline bool qkl_plan(const size_t* pos, uint32_t k, uint32_t n, qkl_geo& g) {
+  bool tgt[64] = {};
+  for (uint32_t b = 0; b < k; ++b) tgt[pos[b]] = true;
+  uint32_t h = 0, free = 0, gb[4];
+  while (free < 4 && h < n) {
+    if (!tgt[h]) gb[free++] = h;
+    ++h;
+  }
+  if (free < 4) return false;
+  g = qkl_geo{};
+  g.h = h;
+  int hidx[64];
+  for (uint32_t p = h; p < n; ++p)
+    if (tgt[p]) {
+      hidx[p] = (int)g.nhi;
+      g.hi[g.nhi++] = p;
+    }
+  for (uint32_t c = 0; c < (1u << g.nhi); ++c) {
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < g.nhi; ++i)
+      if ((c >> i) & 1u) o |= (uint64_t)1 << g.hi[i];
+    g.choff[c] = o;
+  }
+  const uint32_t C = 1u << k;
+  for (uint32_t ci = 0; ci < C; ++ci) {
+    uint32_t lo = 0, c = 0;
+    for (uint32_t b = 0; b < k; ++b) {
+      if (!((ci >> (k - 1 - b)) & 1u)) continue;
+      if (pos[b] < h) lo |= 1u << pos[b];
+      else c |= 1u << hidx[pos[b]];
+    }
+    g.eoff[ci] = (c << h) | lo;
+  }
+  for (uint32_t jj = 0; jj < 16; ++jj) {
+    uint32_t e = 0;
+    for (int b = 0; b < 4; ++b)
+      if ((jj >> b) & 1u) e |= 1u << gb[b];
+    g.eg[jj] = e;
+  }
+  g.ntiles = (uint64_t)1 << (n - k - 4);
+  return true;
+}
+
 }  // namespace qdc
 
 namespace qdc {
@@ -272,6 +429,29 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   const double bytes = 2.0 * state_bytes(n);
   const real* buf = ring.dev[slot];
   const char* e;
+  // LDS-staged tiles when at least QDC_QK_LDS targets sit among the five lowest qubits (0:
+  // never).  Measured at n = 28 f32 (tools/qk_pos_probe.py, profiles/r4w_qk_lds_ab.log): targets
+  // 1..k 0.60 / 0.58 / 0.45 -> 0.68 / 0.67 / 0.63 of HBM at k = 3 / 4 / 5, bench.py's random
+  // placements k = 4 0.58 -> 0.66, k = 5 0.57 -> 0.63; one low target at k = 3 is faster
+  // through k_qk's paired groups (0.72 against 0.62), so k = 3 stages from two
+  uint32_t nlow = 0;
+  for (uint32_t b = 0; b < k; ++b) nlow += pos[b] < 5;
+  int lds_min = k == 3 ? 2 : 1;
+  if (const char* el = getenv("QDC_QK_LDS")) lds_min = atoi(el);
+  qkl_geo lg;
+  if (lds_min > 0 && (int)nlow >= lds_min && qkl_plan(pos, k, n, lg)) {
+    // tiles per wave iteration: 8 KiB per wave in f32 at k >= 4
+    constexpr bool f64 = sizeof(real) == 8;
+    const uint64_t nbl = k == 3 ? (f64 ? 2 : 4) : (k == 5 && f64) ? 1 : 2;
+    const uint64_t lw = (lg.ntiles + nbl - 1) / nbl;
+    const uint32_t lgrid = (uint32_t)std::min<uint64_t>((lw + 3) / 4, gmax);
+    if (k == 3) e = c.launch_block("qk3", bytes, k_qkl<3, f64 ? 2 : 4>, lgrid, 256u, s, buf, lg);
+    else if (k == 4) e = c.launch_block("qk4", bytes, k_qkl<4, 2>, lgrid, 256u, s, buf, lg);
+    else e = c.launch_block("qk5", bytes, k_qkl<5, f64 ? 1 : 2>, lgrid, 256u, s, buf, lg);
+    QDC_TRY(e);
+    QDC_HIP(hipEventRecord(ring.done[slot], c.stream));
+    return nullptr;
+  }
 #define QDC_QK_LAUNCH(KK, PP, NB3)                                                              \
   e = pfwide ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, 2 * (NB3), true>, grid, 256u, s, buf, g) \
       : pf   ? c.launch_block("qk" #KK, bytes, k_qk<KK, PP, (NB3), true>, grid, 256u, s, buf, g) \

@@ -1,7 +1,7 @@
 """Dense k-qubit gates (SURVEY.md §8 f rank 4; include/qdc/dense.h, csrc/qdc_qk.hpp): the MFMA
 kernel (k = 3..5) and the routed k = 1, 2 paths against the oracle's apply_qk_gate (pinned to
 the reference's q1/q2 oracles in tests/test_oracle.py), at every layout class of the targets
-(in-chunk qubit 0, lane bits, far bits, unsorted positions); the panics; and at n = 28 the
+(in-chunk qubit 0, lane bits, far bits, unsorted positions), through both kernels; the panics; and at n = 28 the
 size-independent round trip U then U^+ (f32 1e-5 / f64 1e-12 norm-relative)."""
 import numpy as np
 import pytest
@@ -40,6 +40,28 @@ def test_qk_gate_matches_oracle(prec, k):
         want = O.apply_qk_gate(psi.astype(DT[prec]).astype(np.complex128), u.astype(DT[prec]), pos)
         err = np.abs(got - want).max() / np.abs(want).max()
         assert err < TOL[prec] * 8, (pos, err)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("k", [3, 4, 5])
+@pytest.mark.parametrize("lds", ["0", "1"])
+def test_qk_gate_both_kernels_every_placement(monkeypatch, prec, k, lds):
+    """k_qk (QDC_QK_LDS=0) and the LDS-staged tiles (k_qkl, QDC_QK_LDS=1: every gate with a
+    target below qubit 5) at placements that put 0..k targets among the tile's low bits, the
+    highest qubit included, and at n = k + 4 (one tile)."""
+    monkeypatch.setenv("QDC_QK_LDS", lds)
+    rng = np.random.default_rng(40 + k)
+    for n, pos in ((17, list(range(k))), (17, list(range(1, k + 1))[::-1]),
+                   (17, [4] + list(range(16, 16 - (k - 1), -1))), (17, [0, 5] + list(range(8, 8 + k - 2))),
+                   (17, [2, 16] + list(range(10, 10 + k - 2))), (k + 4, list(range(k + 3, 3, -1))),
+                   (k + 4, [0] + list(range(k + 3, k + 3 - (k - 1), -1)))):
+        psi = O.random_state(rng, n)
+        u = O.haar_unitary(rng, 1 << k)
+        t = tensor(prec, psi)
+        t.apply_qk_gate(u.astype(DT[prec]), pos)
+        want = O.apply_qk_gate(psi.astype(DT[prec]).astype(np.complex128), u.astype(DT[prec]), pos)
+        err = np.abs(t.get_cpu_state_copy() - want).max() / np.abs(want).max()
+        assert err < TOL[prec] * 8, (n, pos, err)
 
 
 @pytest.mark.parametrize("k", [3, 5])
