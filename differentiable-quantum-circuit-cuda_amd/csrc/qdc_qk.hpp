@@ -200,7 +200,7 @@ __device__ __forceinline__ uint32_t qkl_swz(uint32_t e) {
   return e ^ (((e / PE) % (PE / VEC)) * VEC);
 }
 
-template <int K, int NB>
+template <int K, int NB, bool PF = false>
 __global__ __launch_bounds__(256) void k_qkl(cx* __restrict__ s, const real* __restrict__ aop,
                                              qkl_geo g) {
   constexpr int C = 1 << K, T = C / 8, S = C / 2, M = C / 4;
@@ -235,9 +235,9 @@ __global__ __launch_bounds__(256) void k_qkl(cx* __restrict__ s, const real* __r
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   cx* cell = reinterpret_cast<cx*>(&lds[w][0][0]);
-  for (uint64_t t0 = wave * NB; t0 < g.ntiles; t0 += nwaves * NB) {
-    uint64_t base[NB];
-    chunk raw[NB][NP];
+  uint64_t base[NB];
+  chunk raw[NB][NP];
+  auto load = [&](uint64_t t0) __attribute__((always_inline)) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       base[nb] = (t0 + nb) << g.h;
@@ -248,11 +248,24 @@ __global__ __launch_bounds__(256) void k_qkl(cx* __restrict__ s, const real* __r
           raw[nb][i] = ldc(reinterpret_cast<const chunk*>(s + base[nb] + po[i]));
       }
     }
+  };
+  const uint64_t step = nwaves * NB;
+  uint64_t t0 = wave * NB;
+  if (t0 < g.ntiles) load(t0);
+  while (t0 < g.ntiles) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int i = 0; i < NP; ++i) lds[w][nb][pc[i]] = raw[nb][i];
     __builtin_amdgcn_wave_barrier();
+    uint64_t cbase[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) cbase[nb] = base[nb];
+    const uint64_t cur = t0;
+    t0 += step;
+    // PF: the staged tiles free the load registers, so the next tiles' loads are issued now and
+    // fly while these run on the matrix cores
+    if (PF && t0 < g.ntiles) load(t0);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       cx x[M];
@@ -278,12 +291,13 @@ __global__ __launch_bounds__(256) void k_qkl(cx* __restrict__ s, const real* __r
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
-      if (t0 + nb < g.ntiles) {
+      if (cur + nb < g.ntiles) {
 #pragma unroll
         for (int i = 0; i < NP; ++i)
-          stc(reinterpret_cast<chunk*>(s + base[nb] + po[i]), lds[w][nb][pc[i]]);
+          stc(reinterpret_cast<chunk*>(s + cbase[nb] + po[i]), lds[w][nb][pc[i]]);
       }
     __builtin_amdgcn_wave_barrier();  // the next tiles overwrite these cells
+    if (!PF && t0 < g.ntiles) load(t0);
   }
 }
 
@@ -442,12 +456,25 @@ inline const char* apply_qk(Ctx& c, cx* s, const qdc_complex* U, const size_t* p
   if (lds_min > 0 && (int)nlow >= lds_min && qkl_plan(pos, k, n, lg)) {
     // tiles per wave iteration: 8 KiB per wave in f32 at k >= 4
     constexpr bool f64 = sizeof(real) == 8;
-    const uint64_t nbl = k == 3 ? (f64 ? 2 : 4) : (k == 5 && f64) ? 1 : 2;
+    // QDC_QKL_VAR (A/B): 0 not pipelined, 1 pipelined, 2 pipelined with half the tiles at k = 5.
+    // Same-box A/B (profiles/r4z_qkl_pf_ab.log, bench.py's placements, two repeats): k = 4
+    // 0.648 / 0.640 -> 0.653 / 0.652, k = 5 0.617 / 0.612 -> 0.634 / 0.635 (2: 0.621 / 0.624),
+    // k = 3 neutral
+    int var = 1;
+    if (const char* ev = getenv("QDC_QKL_VAR")) var = atoi(ev);
+    const bool lpf = var != 0;
+    const bool half5 = var == 2 || f64;
+    const uint64_t nbl = k == 3 ? (f64 ? 2 : 4) : (k == 5 && half5) ? 1 : 2;
     const uint64_t lw = (lg.ntiles + nbl - 1) / nbl;
     const uint32_t lgrid = (uint32_t)std::min<uint64_t>((lw + 3) / 4, gmax);
-    if (k == 3) e = c.launch_block("qk3", bytes, k_qkl<3, f64 ? 2 : 4>, lgrid, 256u, s, buf, lg);
-    else if (k == 4) e = c.launch_block("qk4", bytes, k_qkl<4, 2>, lgrid, 256u, s, buf, lg);
-    else e = c.launch_block("qk5", bytes, k_qkl<5, f64 ? 1 : 2>, lgrid, 256u, s, buf, lg);
+#define QDC_QKL_LAUNCH(KK, NBB) \
+  e = lpf ? c.launch_block("qk" #KK, bytes, k_qkl<KK, NBB, true>, lgrid, 256u, s, buf, lg) \
+          : c.launch_block("qk" #KK, bytes, k_qkl<KK, NBB>, lgrid, 256u, s, buf, lg)
+    if (k == 3) QDC_QKL_LAUNCH(3, f64 ? 2 : 4);
+    else if (k == 4) QDC_QKL_LAUNCH(4, 2);
+    else if (half5) QDC_QKL_LAUNCH(5, 1);
+    else QDC_QKL_LAUNCH(5, 2);
+#undef QDC_QKL_LAUNCH
     QDC_TRY(e);
     QDC_HIP(hipEventRecord(ring.done[slot], c.stream));
     return nullptr;
