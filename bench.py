@@ -41,10 +41,14 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--qubits", type=int, default=28)
-    ap.add_argument("--layers", type=int, default=20)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
+                    help="BASELINE.json config: c2 layered random circuit (configs[1] generator, "
+                         "the headline), c4 brickwall (configs[3]), c5 deep random (configs[4])")
+    ap.add_argument("--qubits", type=int, default=None, help="default: the workload's n")
+    ap.add_argument("--layers", type=int, default=None,
+                    help="layers (c2, c4) or gates (c5); default: the workload's")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--seed", type=int, default=24)
+    ap.add_argument("--seed", type=int, default=None, help="default: the workload's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--local-shards", type=int, default=None,
                     help="rehearse the sharded data path on one GPU (G shards, device copies in "
@@ -54,19 +58,51 @@ def parse(argv=None):
                          "on its own stream of device 0 (event-ordered copies in place of RCCL)")
     ap.add_argument("--no-gate-sample", action="store_true",
                     help="skip the single-gate (fusion off) kernel sweep and the other auxiliary samples")
-    ap.add_argument("--cpu-layers", type=int, default=2,
-                    help="layers of the C2 circuit the CPU baseline runs as one whole call")
+    ap.add_argument("--cpu-layers", type=int, default=None,
+                    help="layers of the C2 circuit the CPU baseline's headline call runs "
+                         "(default: the GPU step's, i.e. the whole step)")
     ap.add_argument("--cpu-qubits", type=int, default=None)
     ap.add_argument("--cpu-c3-max-s", type=float, default=120.0,
                     help="time one whole C3 call on the CPU when its projection is below this")
     ap.add_argument("--pmc", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--micro", action="store_true", help="per-kernel bandwidth sweep")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    wl = WORKLOADS[args.workload]
+    args.qubits = wl["qubits"] if args.qubits is None else args.qubits
+    args.layers = wl["layers"] if args.layers is None else args.layers
+    if args.seed is None:
+        args.seed = wl["seed"]
+    return args
 
 
-def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None, devices=None):
-    from quantum_differentiable_circuit import workloads as W  # synthetic C2 workload
-    ins, var = W.layered_circuit(n, layers, seed)
+# BASELINE.json configs with a GPU workload of their own (SURVEY.md §8 d); C1 is the CPU GHZ
+# plumbing check and C3 the f64 VQSE example (bench line's vqse_c3 block)
+WORKLOADS = {
+    "c2": {"qubits": 28, "layers": 20, "seed": 24, "config": "configs[1]",
+           "name": "C2 layered random circuit (configs[1] generator: per layer a Haar q1 var gate "
+                   "on every qubit + Haar q2 var brickwork, DiffQ1Density on every qubit)"},
+    "c4": {"qubits": 30, "layers": 40, "seed": 30, "config": "configs[3]",
+           "name": "C4 brickwall (configs[3]: 40 layers of Haar q2 var gates on (i, i+1), even then "
+                   "odd, DiffQ1Density on every qubit)"},
+    "c5": {"qubits": 33, "layers": 10000, "seed": 33, "config": "configs[4]",
+           "name": "C5 deep random circuit (configs[4]: 10 000 gates, 50 % Haar q1, 35 % Haar q2, "
+                   "15 % diagonal, DiffQ1Density on {0, n/2, n-2, n-1})"},
+}
+
+
+def workload_circuit(workload, n, layers, seed):
+    """(instructions, var_gates) of a BASELINE workload (quantum_differentiable_circuit.workloads)."""
+    from quantum_differentiable_circuit import workloads as W
+    if workload == "c4":
+        return W.brickwall_circuit(n, layers, seed)
+    if workload == "c5":
+        return W.deep_random_circuit(n, layers, seed)
+    return W.layered_circuit(n, layers, seed)
+
+
+def build_circuit(q, n, layers, seed, precision, comm=None, local_shards=None, devices=None,
+                  workload="c2"):
+    ins, var = workload_circuit(workload, n, layers, seed)
     c = q.circuit_class(precision)(n, comm=comm, local_shards=local_shards, devices=devices)
     for kind, pos in ins:
         c._push(kind, *pos)
@@ -200,54 +236,73 @@ def cpu_baseline(args, n):
     rules in C/OpenMP, driven in circuit.rs's order by oracle.OracleCircuit: unfused, one kernel
     per step, uncompute + gradient + pull-back per gate backward, a new state per density
     injection), timed end to end on whole calls:
-      value: one whole forward + backward call of the C2 generator at full n with
-        --cpu-layers layers (default 2: 110 gates) and all of C2's densities, at all threads;
-      full_step: the 20-layer step extrapolated from two measured whole calls (1 and
-        --cpu-layers layers: per-layer slope + the fixed density part), a cross-check;
+      value (c2): one whole forward + backward call of the GPU line's own step — the C2
+        generator at full n with --cpu-layers layers (default: the step's 20) and all of C2's
+        densities — at all threads;
+      two_layer_call: a measured whole 2-layer call (density-heavy: its 28 densities are the
+        same as the step's), a cross-check;
       projection: the per-kind fwd+bwd costs (q1 / q2 / density + injection) timed at sampled
-        positions and projected onto the step's gate mix (how earlier rounds reported it);
-      single_thread: the per-kind projection at one thread (a whole call would take minutes);
-      c3_vqse: one whole C3 loss-and-gradient call (n = 26 f64) when its projection is short."""
+        positions and projected onto the step's gate mix;
+      single_thread: the per-kind projection at one thread (a whole call would take an hour);
+      c3_vqse: one whole C3 loss-and-gradient call (n = 26 f64) when its projection is short.
+    c4 / c5: the per-kind projection of the workload's gate mix at min(n, 30) qubits (a whole
+    C5 call at n = 33 is hours of CPU time and three 64 GiB host states)."""
     # idle OpenMP threads sleep instead of spinning: spinning teams were starved on shared
     # hosts (64-100 ms for a 2 ms kernel in this container); read when libgomp loads
     os.environ.setdefault("OMP_WAIT_POLICY", "passive")
     from oracle.cref import CRefOps
     from quantum_differentiable_circuit import workloads as W
     dt = np.complex64 if args.precision == "f32" else np.complex128
-    ins, _ = W.layered_circuit(n, args.layers, args.seed)
-    n_q1 = sum(1 for k, _ in ins if k == 8)
-    n_q2 = sum(1 for k, _ in ins if k == 1)
-    n_d1 = sum(1 for k, _ in ins if k == 13)
+    ins, _ = workload_circuit(args.workload, n, args.layers, args.seed)
+    n_q1 = sum(1 for k, _ in ins if k == W.VAR_Q1)
+    n_q2 = sum(1 for k, _ in ins if k == W.VAR_Q2)
+    n_dg = sum(1 for k, _ in ins if k == W.VAR_Q2_DIAG)
+    n_d1 = sum(1 for k, _ in ins if k == W.DIFF_Q1_DENSITY)
+    ngates = n_q1 + n_q2 + n_dg
     res = {}
     t_all = time.perf_counter()
     ops = CRefOps(args.precision)
     threads = ops.threads()
+    if args.workload != "c2":
+        nc = min(n, args.cpu_qubits or 30)
+        spread = [0, nc // 2, nc - 1]
+        pairs = [(1, 0), (nc // 2 + 1, nc // 2), (nc - 1, nc - 2)]
+        c = _cref_op_costs(ops, nc, spread, pairs, [0, nc - 1], [], pairs if n_dg else ())
+        step = n_q1 * c["q1"] + n_q2 * c["q2"] + n_dg * c.get("diag", 0.0) + n_d1 * c["dens1"]
+        scale = 2.0 ** (n - nc)  # HBM-bound kernels: time per gate ~ state size
+        wall = time.perf_counter() - t_all
+        return {"value": round(ngates / (step * scale), 6), "unit": "gate-applications/s (fwd+bwd)",
+                "cores": threads, "kind": "port", "s_per_step": round(step * scale, 1),
+                "sample": (f"per-kind projection: the reference's fwd+bwd cost per gate kind "
+                           f"(oracle/cpu_ref.c kernels in circuit.rs order, OpenMP on {threads} "
+                           f"threads) timed at n={nc} on sampled positions, projected onto the "
+                           f"{args.workload} step's gate mix ({n_q1} q1, {n_q2} q2, {n_dg} diag, "
+                           f"{n_d1} densities) and scaled by 2^({n}-{nc}) to n={n}; "
+                           f"{wall:.0f} s of CPU time"),
+                "per_gate_s_at_n": {k: round(v, 4) for k, v in c.items()}, "n_timed": nc}
     # whole calls, measured (one untimed layer first: OpenMP team start-up, page first touch)
     _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), dt)
-    lay = max(2, args.cpu_layers)
-    m1 = _cref_whole_call(ops, n, W.layered_circuit(n, 1, args.seed), dt)
-    mL = _cref_whole_call(ops, n, W.layered_circuit(n, lay, args.seed), dt)
-    g1 = sum(1 for k, _ in m1["ins"] if k in (1, 8))
-    gL = sum(1 for k, _ in mL["ins"] if k in (1, 8))
-    slope = (mL["s"] - m1["s"]) / (lay - 1)
-    full = m1["s"] + (args.layers - 1) * slope
-    res["full_step"] = {"s_per_step": round(full, 2), "value": round((n_q1 + n_q2) / full, 4),
-                        "layer_1_call_s": round(m1["s"], 2), f"layer_{lay}_call_s": round(mL["s"], 2),
-                        "per_layer_s": round(slope, 3),
-                        "method": "t(1 layer) + (layers - 1) x [t(L) - t(1)] / (L - 1) over measured whole calls"}
+    lay = args.cpu_layers or args.layers
+    m2 = _cref_whole_call(ops, n, W.layered_circuit(n, 2, args.seed), dt)
+    g2 = sum(1 for k, _ in m2["ins"] if k in (W.VAR_Q1, W.VAR_Q2))
+    res["two_layer_call"] = {"s": round(m2["s"], 2), "gates": g2,
+                             "value": round(g2 / m2["s"], 4)}
+    mL = m2 if lay == 2 else _cref_whole_call(ops, n, W.layered_circuit(n, lay, args.seed), dt)
+    gL = sum(1 for k, _ in mL["ins"] if k in (W.VAR_Q1, W.VAR_Q2))
     # the per-kind projection (earlier rounds' headline), as a cross-check
     spread = [0, n // 2, n - 1]
     c2 = _cref_op_costs(ops, n, spread, [(p + 1, p) for p in spread[:-1]] + [(n - 1, n - 2)],
                         [0, n - 1], [])
     step = n_q1 * c2["q1"] + n_q2 * c2["q2"] + n_d1 * c2["dens1"]
-    res["projection"] = {"s_per_step": round(step, 2), "value": round((n_q1 + n_q2) / step, 4),
-                         "error_vs_full_step": round((step - full) / full, 4),
+    res["projection"] = {"s_per_step": round(step, 2), "value": round(ngates / step, 4),
                          "per_gate_s": {k: round(v, 4) for k, v in c2.items()}}
+    if lay == args.layers:
+        res["projection"]["error_vs_measured_step"] = round((step - mL["s"]) / mL["s"], 4)
     ops.set_threads(1)
     c2s = _cref_op_costs(ops, n, [n // 2], [(n // 2 + 1, n // 2)], [n // 2], [])
     ops.set_threads(threads)
     step1 = n_q1 * c2s["q1"] + n_q2 * c2s["q2"] + n_d1 * c2s["dens1"]
-    res["single_thread"] = {"value": round((n_q1 + n_q2) / step1, 4), "cores": 1,
+    res["single_thread"] = {"value": round(ngates / step1, 4), "cores": 1,
                             "s_per_step": round(step1, 2), "kind": "per-kind projection",
                             "per_gate_s": {k: round(v, 4) for k, v in c2s.items()}}
     # C3: the VQSE circuit at the example's size, f64
@@ -274,16 +329,17 @@ def cpu_baseline(args, n):
     else:
         res["c3_vqse"]["s_per_loss_grad_call"] = f"not measured: projected {call:.0f} s > --cpu-c3-max-s"
     wall = time.perf_counter() - t_all
+    whole = lay == args.layers
     return {"value": round(gL / mL["s"], 4), "unit": "gate-applications/s (fwd+bwd)",
             "cores": threads, "kind": "port", "s_per_call": round(mL["s"], 2),
             "sample": (f"measured: one whole forward + backward call of the C2 generator at full "
                        f"n={n} {args.precision} with {lay} layers ({gL} gates) and its {n_d1} "
-                       f"densities, the reference's algorithm (oracle/cpu_ref.c kernels in "
-                       f"circuit.rs order: unfused, per-gate uncompute + gradient + pull-back, a "
-                       f"new state per density injection), OpenMP on {threads} threads, timed end "
-                       f"to end; full_step: the {args.layers}-layer step from the 1- and "
-                       f"{lay}-layer calls; projection / single_thread: per-kind costs; "
-                       f"c3_vqse: one whole n=26 f64 VQSE call; {wall:.0f} s of CPU time"),
+                       f"densities" + (" - the GPU line's own step" if whole else "") +
+                       f", the reference's algorithm (oracle/cpu_ref.c kernels in circuit.rs "
+                       f"order: unfused, per-gate uncompute + gradient + pull-back, a new state "
+                       f"per density injection), OpenMP on {threads} threads, timed end to end; "
+                       f"two_layer_call / projection / single_thread: cross-checks; c3_vqse: one "
+                       f"whole n=26 f64 VQSE call; {wall:.0f} s of CPU time"),
             **res}
 
 
@@ -533,16 +589,23 @@ def main():
     elif args.local_streams and args.local_streams > 1:  # the same plumbing, one GPU
         devices = [0] * args.local_streams
     c, ins, vg = build_circuit(q, n, args.layers, args.seed, args.precision, comm,
-                               args.local_shards, devices)
+                               args.local_shards, devices, args.workload)
     ngates = len(vg)
     cots = sigma_z_cotangents(sum(1 for k, _ in ins if k in (12, 13)), c.dtype)
+    wl = WORKLOADS[args.workload]
     remaps = 0
     shards = world if world > 1 else (len(devices) if devices else (args.local_shards or 1))
     if shards > 1:
         instr = [(k, *p) for k, p in ins]
-        f_ops, end = q.plan(n, shards, instr, 1, precision=args.precision)
-        b_ops, _ = q.plan(n, shards, instr, 2, start_phys=end, precision=args.precision)
-        remaps = sum(o["type"] == "remap" for o in f_ops + b_ops)
+        # the mirrored forward's plan; its backward undoes each of its remaps (qdc_circuit.hpp
+        # unremap), unless QDC_MIRROR=0 (the backward plans its own)
+        if os.environ.get("QDC_MIRROR", "1") != "0":
+            f_ops, _ = q.plan(n, shards, instr, 3, precision=args.precision)
+            remaps = 2 * sum(o["type"] == "remap" for o in f_ops)
+        else:
+            f_ops, end = q.plan(n, shards, instr, 1, precision=args.precision)
+            b_ops, _ = q.plan(n, shards, instr, 2, start_phys=end, precision=args.precision)
+            remaps = sum(o["type"] == "remap" for o in f_ops + b_ops)
 
     tw = time.perf_counter()
     for _ in range(args.warmup):
@@ -639,7 +702,7 @@ def main():
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
     gate_kernels = dense_kernels = vqse = abi = None
-    if rank == 0 and world == 1 and not args.no_gate_sample:
+    if rank == 0 and world == 1 and not args.no_gate_sample and args.workload == "c2":
         # auxiliary samples: a failure there is reported in the line, never loses the headline
         def aux(fn, *a):
             try:
@@ -673,9 +736,10 @@ def main():
             "vs_baseline": None,
             "dtype": "c64 (f32)" if args.precision == "f32" else "c128 (f64)",
             "data": "synthetic (seeded Haar-random gates, |0..0> initial state)",
-            "config": {"workload": f"C2 layered random circuit (configs[1] generator) at the "
-                                   f"metric's n={n}, fwd+bwd",
-                       "qubits": n, "layers": args.layers, "gates_per_step": ngates,
+            "config": {"workload": f"{wl['name']} at n={n}, fwd+bwd",
+                       "baseline_config": f"BASELINE.json {wl['config']}", "bench_workload": args.workload,
+                       "qubits": n, ("gates" if args.workload == "c5" else "layers"): args.layers,
+                       "gates_per_step": ngates, "seed": args.seed,
                        "densities_per_step": len(cots), "state_GiB": state_gib,
                        "parallelism": (f"state sharded over {world} GPUs by high qubits, "
                                        f"RCCL all-to-all remaps, one process per GPU") if world > 1 else

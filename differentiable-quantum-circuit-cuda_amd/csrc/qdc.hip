@@ -88,6 +88,9 @@ QDC_API const char* qdc_circuit_push(qdc_circuit* c, int kind, size_t pos2, size
     return qdc::fail("unknown instruction kind %d", kind);
   const bool q1 = qdc::is_q1_gate(kind) || qdc::is_q1_density(kind);
   c->impl.ins.push_back({kind, (uint32_t)pos2, q1 ? 0u : (uint32_t)pos1});
+  // a backward after this push runs the new instruction too: the last forward's mirrored
+  // schedule does not cover it (the backward then schedules itself)
+  c->impl.mrec.valid = false;
   return nullptr;
 }
 
@@ -377,7 +380,9 @@ QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned
   for (size_t i = 0; i < count; ++i) all[i] = {kinds[i], pos2[i], pos1[i]};
   std::vector<qdc::PlanIn> ops;
   std::vector<int> index;
-  qdc::active_ops(all, mode, ops, index);
+  if (mode < QDC_PLAN_RUN || mode > QDC_PLAN_FORWARD_MIRROR) return 0;
+  const bool mirror = mode == QDC_PLAN_FORWARD_MIRROR;
+  qdc::active_ops(all, mirror ? (int)QDC_PLAN_FORWARD : mode, ops, index);
   qdc::QubitMap m;
   m.identity((uint32_t)n, g);
   if (start_phys) {
@@ -385,7 +390,7 @@ QDC_API size_t qdc_plan(size_t n, size_t world, const int* kinds, const unsigned
     for (uint32_t q = 0; q < n; ++q) m.logi[m.phys[q]] = q;
   }
   std::vector<qdc_plan_op> plan;
-  qdc::plan_pass(ops, index, m, plan, mode == QDC_PLAN_BACKWARD);
+  qdc::plan_pass(ops, index, m, plan, mode == QDC_PLAN_BACKWARD, nullptr, mirror);
   for (size_t i = 0; i < plan.size() && i < cap; ++i) out[i] = plan[i];
   if (end_phys)
     for (uint32_t q = 0; q < n; ++q) end_phys[q] = m.phys[q];

@@ -282,9 +282,10 @@ struct Circuit {
   // directions' rules (qdc_fusion.hpp FusionPlanner::mirror) and the backward runs its passes in
   // reverse, uncomputing each stage with exactly the adjoint of the matrix the forward applied —
   // the O(1)-memory uncompute then drifts like the reference's gate-by-gate U, U^dagger sequence
-  // instead of accumulating the rounding of independently formed stage products.  Unsharded
-  // circuits; the backward must follow a forward call with the same gates (else the backward
-  // schedules itself as usual).  On by default (round 4: C5 n = 14 f32 uncompute 4.85x -> 1.4x
+  // instead of accumulating the rounding of independently formed stage products.  Sharded
+  // circuits too (round 5): the forward's remap plan keeps both directions' order relations and
+  // the backward undoes its remaps in reverse (unremap).  The backward must follow a forward call
+  // with the same gates (else the backward schedules itself as usual).  On by default (round 4: C5 n = 14 f32 uncompute 4.85x -> 1.4x
   // the reference's floor; C2 n = 28 f32 ~3.5 % slower, DESIGN.md "Uncompute drift").
   int mirror = 1;
   // one-state one-wave specialized passes relayout through half the LDS buffer when every
@@ -294,7 +295,7 @@ struct Circuit {
   // (qdc_fusion.hpp defer_trailing_q1; QDC_DEFER_Q1)
   int defer_q1 = 1;
   bool mirror_on() const {
-    return mirror && g == 0 && fuse && fuse_max_ops >= 2 && use_rq && (sizeof(real) == 4 || rq64);
+    return mirror && fuse && fuse_max_ops >= 2 && use_rq && (sizeof(real) == 4 || rq64);
   }
   // one-state one-wave five-slot passes on 2^11 tiles (f32): QDC_RW bit 1, or a mirrored forward
   bool rw1() const { return (rq_wave & 2) || mirror_on(); }
@@ -657,6 +658,33 @@ struct Circuit {
     layout.apply(r.victims);
     return nullptr;
   }
+  // The inverse of remap(r): the all-to-all first (its block exchange, block j of shard s <->
+  // block s of shard j, is its own inverse), then the pack's inverse permutation.  A mirrored
+  // reverse sweep undoes the forward's remaps in reverse order, so each of its passes finds the
+  // physical layout its forward pass ran in.
+  const char* unremap(const qdc_plan_op& r, bool with_bwd) {
+    const uint32_t low = nl - g;
+    const size_t chunk = (size_t)1 << low;
+    for (int which = 0; which < (with_bwd ? 2 : 1); ++which) {
+      std::vector<cx*> send(sh.size()), recv(sh.size());
+      for (size_t s = 0; s < sh.size(); ++s) {
+        send[s] = which == 0 ? sh[s].state : sh[s].bwd;
+        recv[s] = sh[s].scratch;
+      }
+      QDC_TRY(ex.alltoall(sh, send, recv, chunk));
+      for (size_t s = 0; s < sh.size(); ++s) {
+        cx*& buf = which == 0 ? sh[s].state : sh[s].bwd;
+        if (r.pack) {
+          QDC_TRY(sh[s].c().use());
+          QDC_TRY(pack(sh[s].c(), sh[s].scratch, buf, r.victims, g, nl, true));
+        } else {
+          std::swap(buf, sh[s].scratch);
+        }
+      }
+    }
+    layout.unapply(r.victims);
+    return nullptr;
+  }
 
   std::vector<qdc_plan_op> plan(int mode) const {
     std::vector<PlanIn> ops;
@@ -664,7 +692,10 @@ struct Circuit {
     active_ops(ins, mode, ops, index);
     QubitMap m = layout;
     std::vector<qdc_plan_op> out;
-    plan_pass(ops, index, m, out, mode == QDC_PLAN_BACKWARD, &inexact);
+    // a mirrored forward's remap plan keeps both directions' order relations (its reverse is
+    // the backward's plan)
+    plan_pass(ops, index, m, out, mode == QDC_PLAN_BACKWARD, &inexact,
+              mode == QDC_PLAN_FORWARD && mirror_on());
     return out;
   }
 
@@ -680,6 +711,7 @@ struct Circuit {
     std::vector<uint32_t> grad_slots;  // reduction slot of each reduction op, in op order
     bool rq = false;   // register-resident pass (qdc_rq.hpp): k_rq, ops include relayouts
     bool s5 = false;   // rq with five register slots (k_rw<true, 2, false, 1, true>)
+    bool inv = false;  // a remap (type 1) run backwards: a mirrored backward undoing the forward's remap
     uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
     uint32_t tbits = 0;  // amplitude bits of the tile
     // specialized kernel of a five-slot reverse pass or a one-state forward pass (qdc_jit.hpp): name, source, function
@@ -708,7 +740,7 @@ struct Circuit {
     const std::vector<Item>& F = mrec.items;
     for (size_t k = F.size(); k-- > 0;) {
       const Item& f = F[k];
-      if (f.type != 0 && f.type != 2) return false;  // remaps: unsharded circuits only
+      if (f.type != 0 && f.type != 1 && f.type != 2) return false;
       auto sigma = [&](uint32_t p) {
         for (const auto& sw : f.swaps) {
           if (p == sw.first) p = sw.second;
@@ -733,9 +765,10 @@ struct Circuit {
         for (uint32_t r = 0; r < (uint32_t)FMAX_ROWS; ++r) b.hb[r] = f.hb[r];
         return b;
       };
-      if (f.type != 2) {
+      if (f.type != 2) {  // a single op, or a remap undone (unremap)
         Item b;
         b.type = f.type;
+        b.inv = f.type == 1;
         b.ops.push_back(push(f.ops[0]));
         items.push_back(std::move(b));
         continue;
@@ -2027,7 +2060,7 @@ struct Circuit {
       }
       const qdc_plan_op& op = pl[item.ops[0]];
       if (op.type == QDC_PLAN_REMAP) {
-        QDC_TRY(remap(op, have_bwd));
+        QDC_TRY(item.inv ? unremap(op, have_bwd) : remap(op, have_bwd));
         continue;
       }
       const Instr& in = ins[op.instr];

@@ -786,16 +786,20 @@ inline const char* elementwise_count(Ctx& c, const cx* src, cx* dst, uint64_t co
   return c.launch("reduce_sum", 0.0, k_elementwise<OP>, grid, src, dst, count, it, (uint64_t)0);
 }
 
-// remap pack of one shard of nl local qubits (victims: ascending amplitude positions >= 1)
+// remap pack of one shard of nl local qubits (victims: ascending amplitude positions >= 1);
+// unpack: its inverse (victim blocks scattered back to the victim bits)
 inline const char* pack(Ctx& c, const cx* src, cx* dst, const unsigned* victims, uint32_t g,
-                        uint32_t nl) {
+                        uint32_t nl, bool unpack = false) {
   packgeo pg{};
   pg.nchunks = nchunks_of(nl);
   pg.lowc = (nl - g) - LV;
   pg.g = g;
   for (uint32_t k = 0; k < g; ++k) pg.vc[k] = victims[k] - LV;
   const uint32_t grid = (uint32_t)((pg.nchunks + BLOCK - 1) / BLOCK);
-  return c.launch("remap_pack", 2.0 * state_bytes(nl), k_pack, grid,
+  if (unpack)
+    return c.launch("remap_unpack", 2.0 * state_bytes(nl), k_pack<true>, grid,
+                    reinterpret_cast<const chunk*>(src), reinterpret_cast<chunk*>(dst), pg);
+  return c.launch("remap_pack", 2.0 * state_bytes(nl), k_pack<false>, grid,
                   reinterpret_cast<const chunk*>(src), reinterpret_cast<chunk*>(dst), pg);
 }
 

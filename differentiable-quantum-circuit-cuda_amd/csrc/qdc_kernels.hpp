@@ -1270,7 +1270,10 @@ struct packgeo {
   uint32_t vc[8];  // victim chunk bits, ascending
 };
 
+// UNPACK: the inverse permutation, dst[expand(o)] = src[o] (a mirrored reverse sweep undoing a
+// forward remap, qdc_circuit.hpp unremap).
 #ifndef QDC_SPEC_TU  // (not in the specialized kernels' translation units)
+template <bool UNPACK>
 __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
                                                 chunk* __restrict__ dst, packgeo pg) {
   const uint64_t o = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -1279,7 +1282,10 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
   uint64_t idx = o & ((1ull << pg.lowc) - 1ull);
   for (uint32_t k = 0; k < pg.g; ++k) idx = insert_zero(idx, pg.vc[k]);
   for (uint32_t k = 0; k < pg.g; ++k) idx |= ((j >> k) & 1ull) << pg.vc[k];
-  stc(dst + o, ldc(src + idx));
+  if constexpr (UNPACK)
+    stc(dst + idx, ldc(src + o));
+  else
+    stc(dst + o, ldc(src + idx));
 }
 #endif  // QDC_SPEC_TU
 

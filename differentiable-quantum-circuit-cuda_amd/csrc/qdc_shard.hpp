@@ -54,6 +54,23 @@ struct QubitMap {
     for (uint32_t q = 0; q < n; ++q) phys[q] = np[phys[q]];
     for (uint32_t q = 0; q < n; ++q) logi[phys[q]] = q;
   }
+  // The inverse of apply(victims): the layout before that remap (a mirrored reverse sweep
+  // replays the forward's remaps backwards, qdc_circuit.hpp unremap).
+  void unapply(const uint32_t* victims) {
+    const uint32_t L = nl(), low = L - g;
+    std::vector<uint32_t> np(n), inv(n);
+    uint32_t c = 0;
+    for (uint32_t p = 0; p < L; ++p) {
+      bool v = false;
+      for (uint32_t j = 0; j < g; ++j) v |= victims[j] == p;
+      if (!v) np[p] = c++;
+    }
+    for (uint32_t j = 0; j < g; ++j) np[victims[j]] = L + j;
+    for (uint32_t i = 0; i < g; ++i) np[L + i] = low + i;
+    for (uint32_t p = 0; p < n; ++p) inv[np[p]] = p;
+    for (uint32_t q = 0; q < n; ++q) phys[q] = inv[phys[q]];
+    for (uint32_t q = 0; q < n; ++q) logi[phys[q]] = q;
+  }
   // exchange the qubits at physical positions a and b (a permuting fused pass's store)
   void swap_phys(uint32_t a, uint32_t b) {
     const uint32_t la = logi[a], lb = logi[b];
@@ -124,9 +141,11 @@ inline uint32_t order_conflicts(uint32_t c) {
 // ties: highest position (the top local bits need no pack).  On a brickwork circuit the
 // global qubits' light cone grows a couple of qubits per layer, so a remap buys many layers
 // instead of one.  Emits QDC_PLAN_OP / QDC_PLAN_REMAP records; `map` is updated in place.
+// both_dirs: a mirrored forward (its plan, run in reverse, is the reverse sweep's), so ops keep
+// the order relations of both directions.
 inline void plan_pass(const std::vector<PlanIn>& ops, const std::vector<int>& index,
                       QubitMap& map, std::vector<qdc_plan_op>& out, bool backward = false,
-                      const std::vector<uint8_t>* inexact = nullptr) {
+                      const std::vector<uint8_t>* inexact = nullptr, bool both_dirs = false) {
   const uint32_t g = map.g;
   auto qmask = [&](const PlanIn& op) {
     return (1ull << op.a) | (instr_is_q1(op.kind) ? 0ull : (1ull << op.b));
@@ -144,6 +163,7 @@ inline void plan_pass(const std::vector<PlanIn>& ops, const std::vector<int>& in
   for (size_t i = 0; i < ops.size(); ++i) {
     const bool inex = inexact && (size_t)index[i] < inexact->size() && (*inexact)[index[i]];
     cls[i] = order_class(ops[i].kind, backward, inex);
+    if (both_dirs) cls[i] |= order_class(ops[i].kind, !backward, inex);
   }
   std::vector<size_t> rem(ops.size());
   for (size_t i = 0; i < ops.size(); ++i) rem[i] = i;

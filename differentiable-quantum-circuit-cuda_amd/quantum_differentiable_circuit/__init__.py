@@ -192,8 +192,8 @@ class _CircuitBase:
         check(self._lib.qdc_circuit_backward(self._h, ptr(df), ptr(dl), len(dens), ptr(cf),
                                               ptr(cl), len(const_gates), ptr(vf), ptr(vl),
                                               len(var_gates), ptr(out)))
-        # views of this call's private buffer (disjoint slices, like the reference's fresh arrays)
-        return [out[sl] for sl in self._grad_slices()]
+        # one array per gate that owns its data, as the reference returns (circuit.rs:429)
+        return [out[sl].copy() for sl in self._grad_slices()]
 
     # --- instruction metadata (kept on the Python side for output splitting) -----------
     def _out_kinds(self, mode):
@@ -329,7 +329,8 @@ def unpermute(physical: np.ndarray, phys) -> np.ndarray:
 def plan(qubits_number, world, instructions, mode, start_phys=None, precision=None):
     """The sharding planner of the native runtime (qdc_plan, host only): returns
     (ops, end_phys); ops are dicts {"type": "op"|"remap", ...}.  mode: 0 run, 1 forward,
-    2 backward.  `instructions` = [(kind, pos2[, pos1])]."""
+    2 backward, 3 mirrored forward (ops keep both directions' order relations: its plan run in
+    reverse, every remap undone, is the backward's).  `instructions` = [(kind, pos2[, pos1])]."""
     lib = load(precision or default_precision())
     m = len(instructions)
     kinds = (C.c_int * m)(*[int(i[0]) for i in instructions])

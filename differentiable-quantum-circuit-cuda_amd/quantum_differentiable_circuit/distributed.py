@@ -62,7 +62,18 @@ def process_start_time() -> float:
 
 
 _ID_LEN = 128
-_FMT = "<dq64s"  # after the id: rank 0's start time, process id and host name
+# after the id: rank 0's start time, process id, PID-namespace identity and host name
+_FMT = "<dqQ64s"
+
+
+def pid_namespace() -> int:
+    """Identity of this process's PID namespace (the inode of /proc/self/ns/pid; 0 if unknown).
+    Ranks may share a host name (a shared UTS namespace) but not a PID namespace (containers
+    with a mounted /tmp): rank 0's pid is then meaningless to them."""
+    try:
+        return os.stat("/proc/self/ns/pid").st_ino
+    except OSError:
+        return 0
 
 
 def _alive(pid: int) -> bool:
@@ -85,6 +96,7 @@ def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: fl
     path = Path(path)
     start = process_start_time() if start is None else start
     host = os.uname().nodename.encode()[:64]
+    ns = pid_namespace()
     if rank == 0:
         try:
             path.unlink()  # an earlier launch's file: gone before this launch's id appears
@@ -92,7 +104,7 @@ def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: fl
             pass
         raw = make_id()
         tmp = path.with_name(path.name + f".tmp{os.getpid()}")
-        tmp.write_bytes(raw + struct.pack(_FMT, start, os.getpid(), host))
+        tmp.write_bytes(raw + struct.pack(_FMT, start, os.getpid(), ns, host))
         os.replace(tmp, path)
         return raw
     t0 = time.monotonic()
@@ -100,8 +112,9 @@ def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: fl
         try:
             data = path.read_bytes()
             if len(data) == _ID_LEN + struct.calcsize(_FMT):
-                t_root, pid, h = struct.unpack(_FMT, data[_ID_LEN:])
-                live = h.rstrip(b"\0") != host or _alive(pid)
+                t_root, pid, ns_root, h = struct.unpack(_FMT, data[_ID_LEN:])
+                same = h.rstrip(b"\0") == host and ns_root == ns and ns != 0
+                live = not same or _alive(pid)
                 if abs(t_root - start) <= skew and live:
                     return data[:_ID_LEN]
         except FileNotFoundError:

@@ -169,7 +169,14 @@ const char* qdc_circuit_get_range(qdc_circuit* c, int which, int shard, size_t o
                                   qdc_complex* host, size_t len);
 
 /* ---- the sharding planner (host only, no GPU) ---------------------------------------- */
-enum qdc_plan_mode { QDC_PLAN_RUN = 0, QDC_PLAN_FORWARD = 1, QDC_PLAN_BACKWARD = 2 };
+/* QDC_PLAN_FORWARD_MIRROR: a forward whose plan, run in reverse with every remap undone, is the
+ * backward's (mirrored reverse sweeps): ops keep the order relations of both directions. */
+enum qdc_plan_mode {
+  QDC_PLAN_RUN = 0,
+  QDC_PLAN_FORWARD = 1,
+  QDC_PLAN_BACKWARD = 2,
+  QDC_PLAN_FORWARD_MIRROR = 3
+};
 enum qdc_plan_type { QDC_PLAN_OP = 0, QDC_PLAN_REMAP = 1 };
 typedef struct qdc_plan_op {
   int type;             /* QDC_PLAN_OP: run instruction `instr` at physical (pos2, pos1) */

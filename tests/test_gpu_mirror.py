@@ -19,9 +19,9 @@ from quantum_differentiable_circuit import workloads as W
 pytestmark = pytest.mark.gpu
 
 
-def build(prec, n, ins):
+def build(prec, n, ins, **kw):
     import quantum_differentiable_circuit as q
-    c = q.circuit_class(prec)(n)
+    c = q.circuit_class(prec)(n, **kw)
     for kind, pos in ins:
         c._push(kind, *pos)
     return c
@@ -44,6 +44,67 @@ def test_mirror_c5_depth_10k_gates(strict_mirror, prec):
     fl.check("grads", c.backward(fl.cots, [], fl.var), what)
     fl.check("uncomputed", c.get_state(0), what)
     fl.check("bwd", c.get_state(2), what)
+
+
+@pytest.fixture(scope="module")
+def c5_floors():
+    """C5 at depth: one 10k-gate circuit at n = 14 and its floors per precision (shared by the
+    sharded configurations below; each floor costs the reference's algorithm on the CPU)."""
+    n = 14
+    ins, var = W.deep_random_circuit(n, 10000, seed=33)
+    return n, ins, {p: F.Floor(p, n, ins, [], var, run=False) for p in ("f32", "f64")}
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("kw", [{"local_shards": 2}, {"local_shards": 8}, {"devices": [0, 0]}],
+                         ids=["2shards", "8shards", "2streams"])
+def test_c5_depth_10k_gates_sharded(strict_mirror, c5_floors, prec, kw):
+    """Config C5's depth on the sharded path (the path the 8-GPU config runs): the forward's
+    remap plan keeps both directions' order relations and the backward undoes every remap in
+    reverse (qdc_circuit.hpp unremap), so each reverse pass uncomputes with the adjoint of the
+    forward's stage matrix in the layout the forward applied it.  QDC_MIRROR=2: a sharded
+    backward that did not mirror its forward is an error.  Every output within 4x the floor of
+    the reference's own gate-by-gate algorithm (src/circuit.rs:280-392)."""
+    n, ins, fls = c5_floors
+    fl = fls[prec]
+    c = build(prec, n, ins, **kw)
+    phys, world, _, nloc = c.layout()
+    assert world == nloc == len(kw.get("devices", [None])) * kw.get("local_shards", 1)
+    what = f"mirror C5 n={n} 10k {prec} {kw} "
+    fl.check("forward", c.forward([], fl.var), what)
+    fl.check("state", c.get_state(0), what)
+    assert c.layout()[0] != list(range(n)), "the forward must have remapped"
+    fl.check("grads", c.backward(fl.cots, [], fl.var), what)
+    assert c.layout()[0] == list(range(n)), "every remap undone"
+    fl.check("uncomputed", c.get_state(0), what)
+    fl.check("bwd", c.get_state(2), what)
+
+
+def test_push_between_forward_and_backward():
+    """A Diff density pushed after the forward runs in the backward (the mirrored record of the
+    forward no longer covers the circuit: the backward schedules itself), as in the reference,
+    whose backward walks every instruction from the forward's final state."""
+    import quantum_differentiable_circuit as q
+    n = 12
+    ins, var = O.layered_circuit(n, layers=3, seed=8)
+    dt = np.complex64
+    c = build("f32", n, ins)
+    o = O.OracleCircuit(n)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    vg = [np.ascontiguousarray(g, dtype=dt) for g in var]
+    v128 = [g.astype(np.complex128) for g in vg]
+    d = c.forward([], vg)
+    od = o.forward([], v128)
+    c.get_q2_dens_op_with_grad(3, 7)
+    o.add(O.DIFF_Q2_DENSITY, 3, 7)
+    cots = F.sigma_z_cots(list(d) + [np.zeros((4, 4))], dt)
+    cots[-1] = np.ascontiguousarray(np.arange(16).reshape(4, 4) / 16.0 + 0.5j, dtype=dt)
+    g = np.concatenate(c.backward(cots, [], vg))
+    want = np.concatenate(o.backward([x.astype(np.complex128) for x in cots], [], v128))
+    assert F.normrel(g, want) < 1e-5, F.normrel(g, want)
+    assert len(od) == len(d)
+    del q
 
 
 @pytest.mark.parametrize("prec", ["f32", "f64"])

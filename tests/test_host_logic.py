@@ -106,15 +106,20 @@ def test_rccl_id_bootstrap_ignores_a_dead_launch(tmp_path):
     dead.wait()
     now = D.process_start_time()
     host = os.uname().nodename.encode()
-    path.write_bytes(b"s" * 128 + struct.pack(D._FMT, now, dead.pid, host))
+    ns = D.pid_namespace()
+    path.write_bytes(b"s" * 128 + struct.pack(D._FMT, now, dead.pid, ns, host))
     with pytest.raises(TimeoutError):
         D.exchange_id(1, path, None, timeout=0.3, start=now)
     # a live rank 0 on another host (a shared id path) is taken on its start time alone
-    path.write_bytes(b"o" * 128 + struct.pack(D._FMT, now, dead.pid, b"elsewhere"))
+    path.write_bytes(b"o" * 128 + struct.pack(D._FMT, now, dead.pid, ns, b"elsewhere"))
     assert D.exchange_id(1, path, None, timeout=1, start=now) == b"o" * 128
+    # the same host name but another PID namespace (containers sharing a UTS namespace and
+    # /tmp): the pid means nothing here, the start time alone decides
+    path.write_bytes(b"p" * 128 + struct.pack(D._FMT, now, dead.pid, ns + 1, host))
+    assert D.exchange_id(1, path, None, timeout=1, start=now) == b"p" * 128
     assert D.exchange_id(0, path, lambda: b"n" * 128, start=now) == b"n" * 128
     assert D.exchange_id(1, path, None, timeout=1, start=now) == b"n" * 128
     # an id of a launch that started long before this rank: rejected
-    path.write_bytes(b"x" * 128 + struct.pack(D._FMT, now - 1000, os.getpid(), host))
+    path.write_bytes(b"x" * 128 + struct.pack(D._FMT, now - 1000, os.getpid(), ns, host))
     with pytest.raises(TimeoutError):
         D.exchange_id(1, path, None, timeout=0.3, start=now)

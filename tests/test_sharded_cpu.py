@@ -54,6 +54,32 @@ def remap(shard, r, nl, world):
     return out.view(torch.complex128).numpy().copy()
 
 
+def unpack(shard, victims, nl):
+    """The inverse of pack: dst[expand(o)] = src[o] (k_pack<true>)."""
+    g = len(victims)
+    low = nl - g
+    o = np.arange(1 << nl)
+    idx = o & ((1 << low) - 1)
+    for v in victims:
+        lo = idx & ((1 << v) - 1)
+        idx = ((idx - lo) << 1) | lo
+    j = o >> low
+    for k, v in enumerate(victims):
+        idx |= ((j >> k) & 1) << v
+    out = np.empty_like(shard)
+    out[idx] = shard
+    return out
+
+
+def unremap(shard, r, nl, world):
+    """The runtime's unremap (csrc/qdc_circuit.hpp): the all-to-all, then the inverse pack."""
+    t = torch.from_numpy(np.ascontiguousarray(shard)).view(torch.float64)
+    out = torch.empty_like(t)
+    dist.all_to_all_single(out, t)
+    got = out.view(torch.complex128).numpy().copy()
+    return unpack(got, r["victims"], nl) if r["pack"] else got
+
+
 def allreduce(x):
     t = torch.from_numpy(np.ascontiguousarray(np.asarray(x, np.complex128))).view(torch.float64)
     dist.all_reduce(t)
@@ -68,14 +94,16 @@ def apply(shard, kind, p2, p1, g):
     return O.apply_q2_gate_diag(shard, g, p2, p1)
 
 
-def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
+def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn, mirror=False):
     import quantum_differentiable_circuit as q
     g = world.bit_length() - 1
     nl = n - g
     instr = [(k, *p) for k, p in ins]
     shard = psi0[rank << nl:(rank + 1) << nl].astype(np.complex128).copy()
-    # forward (Circuit::forward): gates + Diff densities
-    ops, phys_end = q.plan(n, world, instr, mode=1, precision="f64")
+    # forward (Circuit::forward): gates + Diff densities; mirrored: the plan whose reverse, with
+    # every remap undone, is the backward's (the runtime's mirrored reverse sweeps)
+    ops, phys_end = q.plan(n, world, instr, mode=3 if mirror else 1, precision="f64")
+    fwd_ops = ops
     kinds = [k for k, _ in ins]
     gidx, ci, vi = {}, 0, 0
     for i, k in enumerate(kinds):
@@ -103,14 +131,18 @@ def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
     dens = [allreduce(dens[i]).reshape(int(np.sqrt(dens[i].size)), -1) for i in order]
     cot_of = dict(zip(order, cot_fn(dens)))
     # backward (Circuit::backward): reverse order, starting from the forward's final layout
-    ops, _ = q.plan(n, world, instr, mode=2, start_phys=phys_end, precision="f64")
+    if mirror:
+        ops = [dict(o, undo=True) for o in reversed(fwd_ops)]
+    else:
+        ops, _ = q.plan(n, world, instr, mode=2, start_phys=phys_end, precision="f64")
     bwd = None
     grads = {}
     for op in ops:
         if op["type"] == "remap":
-            shard = remap(shard, op, nl, world)
+            move = unremap if op.get("undo") else remap
+            shard = move(shard, op, nl, world)
             if bwd is not None:
-                bwd = remap(bwd, op, nl, world)
+                bwd = move(bwd, op, nl, world)
             nremap += 1
             continue
         i = op["instr"]
@@ -138,6 +170,8 @@ def run_sharded(n, world, rank, ins, const, var, psi0, cot_fn):
                 grads[i] = O.get_q2_grad_diag(shard, bwd, p2, p1)
         bwd = apply(bwd, k, p2, p1, gate if k in DIAG else O.transpose(gate))
     grads = [allreduce(grads[i]) for i in sorted(grads)]
+    if mirror:  # every remap undone: the uncomputed shard is back in the identity layout
+        assert np.abs(shard - psi0[rank << nl:(rank + 1) << nl]).max() < 1e-10
     return dens, grads, nremap
 
 
@@ -147,7 +181,8 @@ def worker(rank, world, port, case, q_out):
                             world_size=world)
     try:
         n, ins, const, var, psi0, cot_fn = make_case(case)
-        dens, grads, nremap = run_sharded(n, world, rank, ins, const, var, psi0, cot_fn)
+        dens, grads, nremap = run_sharded(n, world, rank, ins, const, var, psi0, cot_fn,
+                                          mirror=case.endswith("_mirror"))
         q_out.put((rank, dens, grads, nremap, None))
     except Exception as e:  # noqa: BLE001
         import traceback
@@ -165,6 +200,7 @@ def sz_cots(dens):
 
 
 def make_case(case):
+    case = case.removesuffix("_mirror")
     if case == "autodiff":
         n = 9
         ins, const, var, _ = O.autodiff_circuit(n, 2, seed=5)
@@ -178,8 +214,11 @@ def make_case(case):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("case", ["autodiff", "layered"])
+@pytest.mark.parametrize("case", ["autodiff", "layered", "autodiff_mirror", "layered_mirror"])
 def test_sharded_plan_execution_matches_oracle(world, case):
+    """`*_mirror`: the mirrored forward plan (qdc_plan mode 3) and, as the backward, that plan
+    reversed with every remap undone (all-to-all, then the inverse pack) — the schedule of the
+    runtime's mirrored reverse sweeps on sharded circuits."""
     ctx = mp.get_context("spawn")
     q_out = ctx.Queue()
     port = free_port()
