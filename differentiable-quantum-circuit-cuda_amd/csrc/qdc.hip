@@ -597,16 +597,55 @@ QDC_API const char* qdc_spec_selftest_batch(unsigned tile_bits, const size_t* co
   return nullptr;
 }
 
+// Ahead-of-time compilation of a circuit's specialized passes (build time, no GPU): a host-only
+// dry run of forward(cg, vg) then backward(dg, cg, vg) on `world` shards builds the same pass
+// programs as the runtime's calls, and every specialized kernel they would launch is compiled
+// into the cache directory (QDC_JIT_DIR).  *kernels: the distinct kernels of the two calls.
+QDC_API const char* qdc_precompile(size_t n, int world, const int* kinds, const unsigned* pos2,
+                                   const unsigned* pos1, size_t count, const qdc_complex* cg,
+                                   const size_t* cl, size_t nc, const qdc_complex* vg,
+                                   const size_t* vl, size_t nv, const qdc_complex* dg,
+                                   const size_t* dl, size_t nd, size_t* kernels) {
+  if (n == 0 || n > 40 || world < 1) return qdc::fail("invalid precompile arguments");
+  qdc::Circuit k;
+  QDC_TRY(k.init_dry((uint32_t)n, world));
+  for (size_t i = 0; i < count; ++i) {
+    const int kind = kinds[i];
+    if (kind < QDC_CONST_Q2 || kind > QDC_DIFF_Q1_DENSITY)
+      return qdc::fail("unknown instruction kind %d", kind);
+    const bool q1 = qdc::is_q1_gate(kind) || qdc::is_q1_density(kind);
+    k.ins.push_back({kind, pos2[i], q1 ? 0u : pos1[i]});
+  }
+  qdc::Flat cf(cg, cl, nc), vf(vg, vl, nv), df(dg, dl, nd);
+  std::vector<qdc_complex> dens(std::max<size_t>(k.output_size(QDC_MODE_FORWARD), 1));
+  QDC_TRY(k.execute(QDC_MODE_FORWARD, cf, vf, dens.data()));
+  std::vector<qdc_complex> grads(std::max<size_t>(k.grad_size(), 1));
+  QDC_TRY(k.backward(df, cf, vf, grads.data()));
+  std::vector<std::string> names, srcs;
+  for (const qdc::SpecEntry* e : k.dry_specs) {
+    names.push_back(e->name);
+    srcs.push_back(e->src);
+  }
+  if (kernels) *kernels = names.size();
+  // (QDC_PRECOMPILE_COUNT=1: count the kernels only)
+  const char* co = getenv("QDC_PRECOMPILE_COUNT");
+  if (names.empty() || (co && atoi(co) != 0)) return nullptr;
+  return qdc::SpecJit::get().compile_only(names, srcs);
+}
+
 QDC_API size_t qdc_jit_stats(double* stats, size_t n) {
   const qdc::JitStats s = qdc::SpecJit::get().counters();
   const bool on = qdc::SpecJit::get().enabled();
-  const double v[8] = {(double)s.compiled, (double)s.waited, (double)s.loaded, s.compile_s,
+  const double v[9] = {(double)s.compiled, (double)s.waited, (double)s.loaded, s.compile_s,
                        s.wait_s, s.ensure_s, on ? 1.0 : 0.0,
-                       (double)qdc::Ctx::spec_launches().load(std::memory_order_relaxed)};
+                       (double)qdc::Ctx::spec_launches().load(std::memory_order_relaxed),
+                       (double)s.queued};
   size_t k = 0;
-  for (; stats && k < n && k < 8; ++k) stats[k] = v[k];
+  for (; stats && k < n && k < 9; ++k) stats[k] = v[k];
   return k;
 }
+
+QDC_API size_t qdc_jit_wait(double timeout_s) { return qdc::SpecJit::get().wait_async(timeout_s); }
 
 QDC_API const char* qdc_jit_dir(char* dir_out, size_t cap) {
   if (!dir_out || cap < 2) return "invalid arguments";

@@ -262,6 +262,10 @@ struct Circuit {
   uint32_t spec_min_qubits = 22;
   uint32_t spec_max = 160;
   int spec_fwd = 1;  // forward (one-state) passes too (QDC_SPEC_FWD)
+  // a program with more than spec_max distinct kernels: its missing kernels are compiled by the
+  // JIT's background thread while the generic kernels run its passes, later calls launch the
+  // specialized ones as their objects appear (QDC_SPEC_ASYNC=0: such programs stay generic)
+  int spec_async = 1;
   // generated kernels by pass program (key: qdc_circuit build_program), with their functions
   std::map<std::vector<uint32_t>, SpecEntry> spec_cache;
   uint64_t spec_epoch = 0;
@@ -300,6 +304,11 @@ struct Circuit {
   // one-state one-wave five-slot passes on 2^11 tiles (f32): QDC_RW bit 1, or a mirrored forward
   bool rw1() const { return (rq_wave & 2) || mirror_on(); }
 
+  // host-only dry run (init_dry): calls stop before their first launch; build_program writes
+  // the pass program into dry_prog and collects the specialized kernels into dry_specs
+  bool dry = false;
+  std::vector<unsigned char> dry_prog;
+  std::vector<SpecEntry*> dry_specs;
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
@@ -345,6 +354,39 @@ struct Circuit {
     ex.comm = comm;
     ex.multi_stream = devices != nullptr && ex.comms.empty() && nlocal > 1;
     layout.identity(n, g);
+    QDC_TRY(read_knobs(world, nlocal));
+    int cur = 0;
+    QDC_HIP(hipGetDevice(&cur));
+    const int ndev = devices ? nlocal : 1;
+    for (int i = 0; i < ndev; ++i) {
+      devs.push_back(std::make_unique<DevRes>());
+      QDC_TRY(devs.back()->ctx.init(devices ? (*devices)[i] : cur));
+    }
+    const size_t bytes = ((size_t)1 << nl) * sizeof(cx);
+    sh.resize(nlocal);
+    for (int s = 0; s < nlocal; ++s) {
+      sh[s].d = devs[devices ? s : 0].get();
+      Ctx& c = sh[s].c();
+      QDC_TRY(c.use());
+      QDC_HIP(hipMalloc(&sh[s].initial, bytes));
+      sh[s].owned.push_back(sh[s].initial);
+      QDC_TRY(alloc_pair(sh[s], bytes));
+      if (g > 0) {
+        QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
+        sh[s].owned.push_back(sh[s].scratch);
+      }
+      // QuantizedTensor::new_standard + clone (circuit.rs:96-102): |0..0> lives on shard 0
+      if (rank0 + s == 0)
+        QDC_TRY(set_standard(c, sh[s].initial, nl));
+      else
+        QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, c.stream));
+      QDC_TRY(copy_initial(sh[s]));
+    }
+    QDC_TRY(sync_all());
+    return nullptr;
+  }
+  // the runtime's QDC_* knobs (environment, read once per circuit)
+  const char* read_knobs(int world, int nlocal) {
     if (const char* e = getenv("QDC_FUSE")) fuse = atoi(e);
     if (const char* e = getenv("QDC_FUSE_MAX_OPS"))
       fuse_max_ops = std::max(1, std::min(atoi(e), FMAX_OPS));
@@ -378,6 +420,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_SPEC_MIN_QUBITS")) spec_min_qubits = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_MAX")) spec_max = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_SPEC_FWD")) spec_fwd = atoi(e);
+    if (const char* e = getenv("QDC_SPEC_ASYNC")) spec_async = atoi(e);
     // the node's hipcc processes shared among the ranks of a multi-process job
     SpecJit::get().set_processes(std::max(1, world / std::max(1, nlocal)));
 
@@ -385,35 +428,24 @@ struct Circuit {
       fuse_lcmin = (uint32_t)std::max(1, std::min(atoi(e), LOWBITS));
     if (const char* e = getenv("QDC_FUSED_BLOCKS"))
       fused_blocks = (uint32_t)std::max(1, std::min(atoi(e), (int)NBMAX));
-    int cur = 0;
-    QDC_HIP(hipGetDevice(&cur));
-    const int ndev = devices ? nlocal : 1;
-    for (int i = 0; i < ndev; ++i) {
-      devs.push_back(std::make_unique<DevRes>());
-      QDC_TRY(devs.back()->ctx.init(devices ? (*devices)[i] : cur));
-    }
-    const size_t bytes = ((size_t)1 << nl) * sizeof(cx);
-    sh.resize(nlocal);
-    for (int s = 0; s < nlocal; ++s) {
-      sh[s].d = devs[devices ? s : 0].get();
-      Ctx& c = sh[s].c();
-      QDC_TRY(c.use());
-      QDC_HIP(hipMalloc(&sh[s].initial, bytes));
-      sh[s].owned.push_back(sh[s].initial);
-      QDC_TRY(alloc_pair(sh[s], bytes));
-      if (g > 0) {
-        QDC_HIP(hipMalloc(&sh[s].scratch, bytes));
-        sh[s].owned.push_back(sh[s].scratch);
-      }
-      // QuantizedTensor::new_standard + clone (circuit.rs:96-102): |0..0> lives on shard 0
-      if (rank0 + s == 0)
-        QDC_TRY(set_standard(c, sh[s].initial, nl));
-      else
-        QDC_HIP(hipMemsetAsync(sh[s].initial, 0, bytes, c.stream));
-      QDC_TRY(copy_initial(sh[s]));
-    }
-    QDC_TRY(sync_all());
     return nullptr;
+  }
+  // A host-only circuit (no device, no state): plans, schedules and pass programs exactly as
+  // execute() / backward() build them, for the specialized kernels compiled ahead of time
+  // (qdc_precompile; dry-run calls return before their first launch).
+  const char* init_dry(uint32_t qubits, int world) {
+    dry = true;
+    n = qubits;
+    const uint32_t gg = log2_exact((size_t)world);
+    if (gg == UINT32_MAX || gg > 8) return fail("the number of shards must be a power of two <= 256");
+    g = gg;
+    if (g > 0 && n < 2 * g + 3)
+      return fail("%u qubits are too few to shard over %d ranks (need >= %u)", n, world, 2 * g + 3);
+    nl = n - g;
+    ex.world = world;
+    ex.nlocal = 1;
+    layout.identity(n, g);
+    return read_knobs(world, world);  // (compiles: this process's full parallelism)
   }
   void destroy() {
     DeviceGuard keep;
@@ -961,7 +993,7 @@ struct Circuit {
                             const std::vector<uint32_t>& var_idx, uint32_t nvar,
                             const std::vector<uint32_t>& out_idx, const Flat* dg) {
     stage_post.clear();
-    if (spec_cache.size() >= 4096) spec_cache.clear();  // bounded; items of this call point into it
+    if (spec_cache.size() >= 4096 && !dry) spec_cache.clear();  // bounded; items of this call point into it
     size_t nops = 0;
     for (size_t ii = 0; ii < items.size(); ++ii)
       if (items[ii].type == 2) nops += items[ii].stages.size();
@@ -975,6 +1007,11 @@ struct Circuit {
         mats_off + (nops * 32 + nfops * (sizeof(rq_layout) / sizeof(cx)) +
                     items.size() * (sizeof(rqio) / sizeof(cx))) *
                        sizeof(cx);
+    if (dry && bytes > prog_cap) {
+      dry_prog.resize(bytes);
+      prog_host = dry_prog.data();
+      prog_cap = bytes;
+    }
     if (bytes > prog_cap) {
       QDC_TRY(sync_all());
       for (auto& d : devs) {
@@ -1369,6 +1406,12 @@ struct Circuit {
         fprintf(stderr, "\n");
       }
     }
+    if (dry) {  // the kernels this call would compile / load
+      for (Item& it : items)
+        if (it.spec && std::find(dry_specs.begin(), dry_specs.end(), it.spec) == dry_specs.end())
+          dry_specs.push_back(it.spec);
+      return nullptr;
+    }
     for (auto& d : devs) {  // prog_host is not rewritten before the call's final sync
       QDC_TRY(d->ctx.use());
       QDC_HIP(hipMemcpyAsync(d->prog_dev, prog_host, mats_off + mo * sizeof(cx),
@@ -1380,8 +1423,8 @@ struct Circuit {
   // specialized passes: circuits of >= spec_min_qubits local qubits (every shard runs the same
   // program; the kernels are loaded on each shard's device)
   bool spec_on() const { return spec_mode > 0 && (spec_mode >= 2 || nl >= spec_min_qubits); }
-  // compile / load the kernels of this program's specialized passes (none when there are more
-  // distinct ones than spec_max: deep random circuits would compile for minutes)
+  // compile / load the kernels of this program's specialized passes (more distinct ones than
+  // spec_max — deep random circuits would compile for minutes — go to the background compiler)
   const char* spec_load(std::vector<Item>& items) {
     if (items.empty()) return nullptr;
     size_t distinct = 0;
@@ -1392,7 +1435,8 @@ struct Circuit {
         ++distinct;
       }
     if (distinct == 0) return nullptr;
-    if (distinct > spec_max) {  // every pass of this call interpreted
+    const bool async = distinct > spec_max;
+    if (async && !spec_async) {  // every pass of this call interpreted
       for (Item& it : items) it.spec = nullptr;
       return nullptr;
     }
@@ -1420,7 +1464,10 @@ struct Circuit {
           break;
         }
       std::vector<hipFunction_t> fns;
-      SpecJit::get().ensure(dev, names, srcs, fns);
+      if (async)  // (what is compiled loads now, the rest compiles in the background)
+        SpecJit::get().ensure_async(dev, names, srcs, fns);
+      else
+        SpecJit::get().ensure(dev, names, srcs, fns);
       for (size_t k = 0; k < todo.size(); ++k)
         if (fns[k]) todo[k]->fn[dev] = fns[k];
     }
@@ -1786,9 +1833,11 @@ struct Circuit {
     ht[0] = hclock::now();
     std::vector<size_t> gidx;
     QDC_TRY(validate_forward(cg, vg, gidx));
-    QDC_TRY(dyn_reset_all());
     const size_t nout = output_count(mode);
-    QDC_TRY(ensure_out(true, std::max<size_t>(nout, 1) * RED));
+    if (!dry) {
+      QDC_TRY(dyn_reset_all());
+      QDC_TRY(ensure_out(true, std::max<size_t>(nout, 1) * RED));
+    }
     // every pass starts from `initial`, which is always in the identity layout
     layout.identity(n, g);
     for (auto& s : sh) {
@@ -1832,6 +1881,17 @@ struct Circuit {
     if (rq_stats)
       fprintf(stderr, "forward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
+    if (dry) {  // the layout the passes leave (permuting passes' swaps, remaps), no launch
+      for (const Item& item : items) {
+        for (const auto& sw : item.swaps) layout.swap_phys(sw.first, sw.second);
+        if (item.type == 1) layout.apply(pl[item.ops[0]].victims);
+      }
+      if (record) {
+        mrec.end_phys = layout.phys;
+        mrec.valid = true;
+      }
+      return nullptr;
+    }
     for (const Item& item : items) {
       if (item.type == 2) {
         QDC_TRY(run_fused(item, false, mats_off, false));
@@ -1970,7 +2030,7 @@ struct Circuit {
     ht[0] = hclock::now();
     std::vector<size_t> gidx;
     QDC_TRY(validate_backward(dg, cg, vg, gidx));
-    QDC_TRY(dyn_reset_all());
+    if (!dry) QDC_TRY(dyn_reset_all());
     const size_t nvar = n_var();
     for (auto& s : sh) {
       if (!s.bwd) {
@@ -1982,7 +2042,7 @@ struct Circuit {
     }
     // slots [0, nvar): per-gate gradients; [nvar, nvar + stages): fused stages' Gamma
     const size_t nslots = std::max<size_t>(2 * nvar, 1);
-    QDC_TRY(ensure_out(false, nslots * RED));
+    if (!dry) QDC_TRY(ensure_out(false, nslots * RED));
     // variable gates met before the first cotangent keep zero gradients (circuit.rs:327-331)
     for (auto& s : sh) {
       QDC_TRY(s.c().use());
@@ -2032,6 +2092,7 @@ struct Circuit {
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
                           (uint32_t)nvar, {}, &dg));
     ht[3] = hclock::now();
+    if (dry) return nullptr;
     if (rq_stats)
       fprintf(stderr, "backward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());

@@ -27,12 +27,19 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cerrno>
+#include <condition_variable>
+#include <csignal>
+#include <cstdlib>
+#include <deque>
 #include <ctime>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -377,17 +384,86 @@ constexpr char JIT_MAGIC[8] = {'Q', 'D', 'C', 'J', 'I', 'T', '2', '\0'};
 
 // counters of this process's specialized-kernel cache (qdc_jit_stats)
 struct JitStats {
+  uint64_t queued = 0;    // kernels waiting for (or in) the background compiler
   uint64_t compiled = 0;  // kernels this process compiled
   uint64_t waited = 0;    // kernels another process was compiling when this one needed them
   uint64_t loaded = 0;    // (kernel, device) loads
   double compile_s = 0, wait_s = 0, ensure_s = 0;
 };
 
+// hipcc children of the background compiler, killed at process exit (an exit during a long
+// background compile leaves no orphaned compiles behind)
+inline std::atomic<pid_t>* jit_children() {
+  static std::atomic<pid_t> pids[16];
+  return pids;
+}
+inline void jit_kill_children() {
+  for (int k = 0; k < 16; ++k) {
+    const pid_t p = jit_children()[k].exchange(0);
+    if (p > 0) kill(p, SIGKILL);
+  }
+}
+
 class SpecJit {
  public:
   static SpecJit& get() {
-    static SpecJit j;
-    return j;
+    // never destroyed: the background compiler's thread may still run at static destruction
+    static SpecJit* j = new SpecJit;
+    return *j;
+  }
+  // Asynchronous form of ensure() for programs with more distinct kernels than a call should
+  // wait for (deep random circuits, Circuit::spec_load): the kernels whose objects exist (this
+  // process, the cache or the prebuilt directory) are loaded on `device` now; the missing ones
+  // are queued for a background thread that compiles them (the same per-kernel locks and cache),
+  // and their passes run the generic kernel until a later call finds the object.  f32
+  // specialized and generic passes are bit-identical, so results do not depend on the timing.
+  void ensure_async(int device, const std::vector<std::string>& names,
+                    const std::vector<std::string>& srcs, std::vector<hipFunction_t>& fns) {
+    std::lock_guard<std::mutex> lk(mu);
+    const double t0 = now();
+    fns.assign(names.size(), nullptr);
+    if (!init()) return;
+    for (size_t i = 0; i < names.size(); ++i) {
+      auto it = loaded.find({device, names[i]});
+      if (it != loaded.end()) {
+        fns[i] = it->second;
+        continue;
+      }
+      if (!image(names[i])) {
+        if (!pending.count(names[i])) {
+          pending.insert(names[i]);
+          queue.push_back({names[i], srcs[i]});
+        }
+        continue;
+      }
+      hipModule_t mod = nullptr;
+      hipFunction_t fn = nullptr;
+      if (hipModuleLoadData(&mod, image(names[i])->data()) != hipSuccess ||
+          hipModuleGetFunction(&fn, mod, names[i].c_str()) != hipSuccess) {
+        (void)hipGetLastError();
+        disable("cannot load " + obj_path(names[i]));
+        fns.assign(names.size(), nullptr);
+        break;
+      }
+      ++stats.loaded;
+      fns[i] = loaded.emplace(std::make_pair(device, names[i]), fn).first->second;
+    }
+    stats.queued = pending.size();
+    if (!queue.empty() && !worker_on && state > 0) {
+      worker_on = true;
+      static bool hooked = (std::atexit(jit_kill_children), true);
+      (void)hooked;
+      std::thread([this] { background(); }).detach();
+    }
+    stats.ensure_s += now() - t0;
+  }
+  // Wait until the background compiler has drained its queue or `timeout_s` passed; returns the
+  // kernels still queued.
+  size_t wait_async(double timeout_s) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait_for(lk, std::chrono::duration<double>(timeout_s < 0 ? 0 : timeout_s),
+                [this] { return !worker_on; });
+    return pending.size();
   }
   // the build fingerprint (0 while specialization is off)
   uint64_t fingerprint() {
@@ -471,9 +547,53 @@ class SpecJit {
 
  private:
   std::mutex mu;
+  std::condition_variable cv;
+  // the background compiler (ensure_async): queued kernels (name, source), their names, whether
+  // its thread runs
+  std::deque<std::pair<std::string, std::string>> queue;
+  std::set<std::string> pending;
+  bool worker_on = false;
+  // Background compiles, one batch of the compile parallelism at a time under the lock (ensure()
+  // and the runtime wait at most one batch: seconds); exits when the queue is empty or
+  // specialization was switched off.
+  void background() {
+    for (;;) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (queue.empty() || state <= 0) {
+          queue.clear();
+          pending.clear();
+          stats.queued = 0;
+          worker_on = false;
+          cv.notify_all();
+          return;
+        }
+        std::vector<std::string> names, srcs;
+        std::vector<size_t> todo;
+        size_t take = (size_t)jobs_now();
+        if (const char* e = getenv("QDC_JIT_ASYNC_JOBS")) take = (size_t)std::max(1, atoi(e));
+        take = std::min(queue.size(), take);
+        for (size_t k = 0; k < take; ++k) {
+          names.push_back(queue.front().first);
+          srcs.push_back(queue.front().second);
+          todo.push_back(k);
+          queue.pop_front();
+        }
+        (void)obtain(names, srcs, todo);  // (a failure disables specialization: loop ends)
+        for (const std::string& nm : names) pending.erase(nm);
+        stats.queued = pending.size();
+      }
+      cv.notify_all();
+    }
+  }
   std::map<std::pair<int, std::string>, hipFunction_t> loaded;
   std::map<std::string, std::vector<char>> images;  // validated code objects (kept for the process)
   std::string hipcc, csrc, inc, dir;
+  // code objects compiled ahead of time (in-tree <pkg>/jit-prebuilt, written by build() through
+  // qdc_precompile; QDC_JIT_PREBUILT names another, 0 none): read-only, searched after `dir`,
+  // validated like the cache's own objects (fingerprint, kernel name, byte hash); used only when
+  // owned by this user and writable by no one else
+  std::string prebuilt;
   uint64_t fp = 0;
   int state = 0;  // 0 unknown, 1 on, -1 off
   int procs = 1;
@@ -495,7 +615,11 @@ class SpecJit {
     auto it = images.find(name);
     if (it != images.end()) return &it->second;
     std::string raw;
-    if (!read_file(obj_path(name), raw) || raw.size() <= sizeof(JitObjHeader)) return nullptr;
+    // the cache directory, then the read-only prebuilt directory (build(): qdc_precompile)
+    if ((!read_file(obj_path(name), raw) || raw.size() <= sizeof(JitObjHeader)) &&
+        (prebuilt.empty() || !read_file(prebuilt + "/" + name + ".qco", raw) ||
+         raw.size() <= sizeof(JitObjHeader)))
+      return nullptr;
     JitObjHeader h;
     memcpy(&h, raw.data(), sizeof h);
     const char* body = raw.data() + sizeof h;
@@ -630,6 +754,15 @@ class SpecJit {
       return false;
     }
     fp = spec_fingerprint(spec_defines(), hipcc + "\n" + ver, sfp);
+    {
+      const char* pe = getenv("QDC_JIT_PREBUILT");
+      std::string p = pe ? std::string(pe) : libdir + "/../jit-prebuilt";
+      struct stat st;
+      if ((pe && std::string(pe) == "0") || p == dir || lstat(p.c_str(), &st) != 0 ||
+          !S_ISDIR(st.st_mode) || st.st_uid != geteuid() || (st.st_mode & 022))
+        p.clear();
+      prebuilt = p;
+    }
     state = 1;
     return true;
   }
@@ -763,6 +896,10 @@ class SpecJit {
     auto reap = [&]() {
       int status = 0;
       const pid_t p = waitpid(run.front().pid, &status, 0);
+      for (int k = 0; k < 16; ++k) {
+        pid_t z = run.front().pid;
+        if (jit_children()[k].compare_exchange_strong(z, 0)) break;
+      }
       Job j = run.front();
       run.erase(run.begin());
       std::string elf;
@@ -814,6 +951,10 @@ class SpecJit {
         if (rc != 0) {
           ok = false;
           continue;
+        }
+        for (int k = 0; k < 16; ++k) {  // (killed at exit if still running)
+          pid_t z = 0;
+          if (jit_children()[k].compare_exchange_strong(z, j.pid)) break;
         }
         run.push_back(j);
         continue;

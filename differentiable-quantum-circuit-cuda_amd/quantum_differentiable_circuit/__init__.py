@@ -469,17 +469,50 @@ def spec_selftest_batch(tile_bits, programs, precision="f32"):
 def jit_stats(precision=None):
     """This process's specialized-kernel cache (qdc_jit_stats): kernels compiled here, kernels
     waited for while another process compiled them, (kernel, device) loads, seconds compiling,
-    waiting and in the cache overall, whether specialization is on, and launches of specialized
-    kernels."""
+    waiting and in the cache overall, whether specialization is on, launches of specialized
+    kernels, and kernels queued for the background compiler."""
     lib = load(precision or default_precision())
-    v = (C.c_double * 8)()
-    k = int(lib.qdc_jit_stats(v, 8))
-    keys = ("compiled", "waited", "loaded", "compile_s", "wait_s", "total_s", "enabled", "launched")
+    v = (C.c_double * 9)()
+    k = int(lib.qdc_jit_stats(v, 9))
+    keys = ("compiled", "waited", "loaded", "compile_s", "wait_s", "total_s", "enabled", "launched",
+            "queued")
     out = {key: float(v[i]) for i, key in enumerate(keys[:k])}
-    for key in ("compiled", "waited", "loaded", "launched"):
+    for key in ("compiled", "waited", "loaded", "launched", "queued"):
         out[key] = int(out[key])
     out["enabled"] = bool(out["enabled"])
     return out
+
+
+def jit_wait(timeout_s=3600.0, precision=None):
+    """Wait for the background compiler (the specialized kernels of programs with more than
+    QDC_SPEC_MAX of them) to drain its queue; returns the kernels still queued."""
+    return int(load(precision or default_precision()).qdc_jit_wait(float(timeout_s)))
+
+
+def precompile(qubits_number, instructions, const_gates, var_gates, grads_wrt_density,
+               world=1, precision=None):
+    """Compile ahead of time (host only, no GPU) every specialized pass kernel that a forward
+    call with these gates, then a backward call with these density cotangents, would launch on a
+    circuit of `instructions` = [(kind, pos2[, pos1])] sharded over `world` ranks: the runtime's
+    own plans, schedules and pass programs, built by a dry run (qdc_precompile).  The kernels go to
+    the cache directory (QDC_JIT_DIR); build() points it at the in-tree prebuilt directory the
+    runtime searches after its own cache.  Returns the number of distinct kernels."""
+    prec = precision or default_precision()
+    lib = load(prec)
+    dt = np.dtype(PRECISIONS[prec])
+    m = len(instructions)
+    kinds = (C.c_int * m)(*[int(i[0]) for i in instructions])
+    a = (C.c_uint * m)(*[int(i[1]) for i in instructions])
+    b = (C.c_uint * m)(*[int(i[2]) if len(i) > 2 else 0 for i in instructions])
+    cf, cl = _flat_gates(const_gates, dt, "const_gates")
+    vf, vl = _flat_gates(var_gates, dt, "var_gates")
+    dens = [_array2(g, dt, "grads_wrt_density") for g in grads_wrt_density]
+    df, dl = _flatten(dens, dt, "grads_wrt_density", "Gradient is not contiguous.")
+    count = C.c_size_t(0)
+    check(lib.qdc_precompile(int(qubits_number), int(world), kinds, a, b, m, ptr(cf), ptr(cl),
+                             len(const_gates), ptr(vf), ptr(vl), len(var_gates), ptr(df), ptr(dl),
+                             len(dens), C.byref(count)))
+    return int(count.value)
 
 
 def jit_dir(precision=None):

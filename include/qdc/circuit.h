@@ -246,12 +246,17 @@ const char* qdc_spec_selftest_batch(unsigned tile_bits, const size_t* counts, si
 int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int two_states,
                   int far_tile, unsigned* out);
 
-/* The specialized-kernel cache of this process (qdc_jit.hpp).  stats[0..7] (up to n) =
+/* The specialized-kernel cache of this process (qdc_jit.hpp).  stats[0..8] (up to n) =
  * {kernels compiled by this process, kernels waited for while another process compiled them,
  * (kernel, device) loads, seconds compiling, seconds waiting, seconds in the cache overall
- * (compile + wait + load), 1 if specialization is on else 0, launches of specialized kernels}.
- * Returns the values written. */
+ * (compile + wait + load), 1 if specialization is on else 0, launches of specialized kernels,
+ * kernels queued for the background compiler}.  Returns the values written. */
 size_t qdc_jit_stats(double* stats, size_t n);
+
+/* Wait up to timeout_s seconds for the background compiler (programs with more distinct
+ * specialized kernels than QDC_SPEC_MAX compile there while generic kernels run their passes)
+ * to drain its queue.  Returns the kernels still queued. */
+size_t qdc_jit_wait(double timeout_s);
 
 /* The cache directory in use (dir_out, cap >= 2): NULL, or an error message when
  * specialization is off (no hipcc, kernel headers changed since the build, no private
@@ -264,6 +269,20 @@ const char* qdc_jit_dir(char* dir_out, size_t cap);
  * the header hash alone.  Returns NULL, or an error message. */
 const char* qdc_spec_fingerprint(const char* defines, const char* compiler, const char* csrc_dir,
                                  unsigned long long* fingerprint, unsigned long long* source_hash);
+
+/* Ahead-of-time compilation (host only, no GPU; build time): a dry run of forward(cg, vg) then
+ * backward(dg, cg, vg) on a circuit of `count` instructions (kinds[], pos2[], pos1[] as
+ * qdc_circuit_push) over `world` shards builds the runtime's own pass programs and compiles
+ * every specialized kernel they would launch into the cache directory (QDC_JIT_DIR).  The
+ * runtime then finds them there, or in the read-only prebuilt directory next to the library
+ * (<pkg>/jit-prebuilt, QDC_JIT_PREBUILT).  *kernels (nullable): the distinct kernels.  Returns
+ * NULL, or an error message. */
+const char* qdc_precompile(size_t qubits_number, int world, const int* kinds,
+                           const unsigned* pos2, const unsigned* pos1, size_t count,
+                           const qdc_complex* const_gates, const size_t* const_lens, size_t n_const,
+                           const qdc_complex* var_gates, const size_t* var_lens, size_t n_var,
+                           const qdc_complex* dens_grads, const size_t* dens_lens, size_t n_dens,
+                           size_t* kernels);
 
 #ifdef __cplusplus
 }

@@ -59,8 +59,11 @@ def test_c4_brickwall_small_vs_oracle():
         fl.check("grads", g, f"C4 n={n} shards={shards} ")
 
 
-def test_c4_brickwall_full_size_sharded_equals_unsharded():
+def test_c4_brickwall_full_size_sharded_equals_unsharded(monkeypatch):
     n, layers = 30, 40
+    # (the unsharded program's 273 distinct pass kernels exceed QDC_SPEC_MAX: keep them generic
+    # rather than compiling in the background while the rest of the suite runs)
+    monkeypatch.setenv("QDC_SPEC_ASYNC", "0")
     ins, var = W.brickwall_circuit(n, layers, seed=30)
     ins16, var16 = W.brickwall_circuit(16, layers, seed=30)
     proxy = F.Floor("f32", 16, ins16, [], var16, run=False).floor  # same generator and depth

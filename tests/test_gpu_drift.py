@@ -68,10 +68,13 @@ def _stream_uncompute_error(c, n, chunk=1 << 26):
     return np.sqrt(s)
 
 
-def test_c5_full_size_10k_gates():
+def test_c5_full_size_10k_gates(monkeypatch):
     n, ngates = 33, 10000
     ins, var = W.deep_random_circuit(n, ngates, seed=33)
     vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
+    # (its >1000 distinct pass kernels would compile in the background for minutes while the
+    # rest of the suite runs: this test checks drift and gradients, and keeps the generic passes)
+    monkeypatch.setenv("QDC_SPEC_ASYNC", "0")
     c = build("f32", n, ins)
     t0 = time.perf_counter()
     d = c.forward([], vg)
