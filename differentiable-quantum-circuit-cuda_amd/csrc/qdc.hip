@@ -633,6 +633,53 @@ QDC_API const char* qdc_precompile(size_t n, int world, const int* kinds, const 
   return qdc::SpecJit::get().compile_only(names, srcs);
 }
 
+// Host-only consistency check of the runtime's forward schedule (tests): plan the forward of a
+// circuit over `world` shards (mirrored when QDC_MIRROR is on, as the runtime does), fuse it
+// (permuting passes relabel later remaps on sharded circuits), then replay the layout: every
+// op's positions must be where its logical qubits are, every remap's victims local and
+// ascending.  *items / *swaps (nullable): the schedule's items and permuting swaps.
+QDC_API const char* qdc_check_schedule(size_t n, int world, const int* kinds, const unsigned* pos2,
+                                       const unsigned* pos1, size_t count, size_t* items_out,
+                                       size_t* swaps_out) {
+  qdc::Circuit k;
+  QDC_TRY(k.init_dry((uint32_t)n, world));
+  for (size_t i = 0; i < count; ++i) {
+    const bool q1 = qdc::is_q1_gate(kinds[i]) || qdc::is_q1_density(kinds[i]);
+    k.ins.push_back({kinds[i], pos2[i], q1 ? 0u : pos1[i]});
+  }
+  k.inexact.assign(k.ins.size(), 0);
+  std::vector<qdc_plan_op> pl = k.plan(QDC_MODE_FORWARD);
+  k.sched_mirror = true;
+  const std::vector<qdc::Circuit::Item> items = k.schedule(pl, false, SIZE_MAX);
+  qdc::QubitMap m;
+  m.identity((uint32_t)n, k.g);
+  size_t nsw = 0;
+  for (const auto& it : items) {
+    for (uint32_t pi : it.ops) {
+      const qdc_plan_op& op = pl[pi];
+      if (op.type == QDC_PLAN_REMAP) {
+        for (uint32_t j = 0; j < op.nvictims; ++j) {
+          if (op.victims[j] == 0 || op.victims[j] >= k.nl || (j > 0 && op.victims[j] <= op.victims[j - 1]))
+            return qdc::fail("remap %u: victims not local, nonzero and ascending", pi);
+        }
+        m.apply(op.victims);
+        continue;
+      }
+      const qdc::Instr& in = k.ins[op.instr];
+      const bool q1 = qdc::is_q1_gate(in.kind) || qdc::is_q1_density(in.kind);
+      if (op.pos2 != m.phys[in.a] || (!q1 && op.pos1 != m.phys[in.b]) || op.pos2 >= k.nl ||
+          op.pos1 >= k.nl)
+        return qdc::fail("plan op %u (instruction %d) at (%u, %u), its qubits at (%u, %u)", pi,
+                         op.instr, op.pos2, op.pos1, m.phys[in.a], q1 ? m.phys[in.a] : m.phys[in.b]);
+    }
+    for (const auto& sw : it.swaps) m.swap_phys(sw.first, sw.second);
+    nsw += it.swaps.size();
+  }
+  if (items_out) *items_out = items.size();
+  if (swaps_out) *swaps_out = nsw;
+  return nullptr;
+}
+
 QDC_API size_t qdc_jit_stats(double* stats, size_t n) {
   const qdc::JitStats s = qdc::SpecJit::get().counters();
   const bool on = qdc::SpecJit::get().enabled();

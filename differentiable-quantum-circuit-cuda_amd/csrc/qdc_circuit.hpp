@@ -272,6 +272,7 @@ struct Circuit {
   int rq_wave = 1;  // one wave per register-resident tile (k_rw; QDC_RW bit 0 two-state, bit 1
                     // one-state, bit 2 two-state with the next tile prefetched into AGPRs)
   int rq_permute = 1;       // gate-only passes permute their tile's qubits (QDC_RQ_PERM)
+  int rq_perm_shard = 1;    // ... on sharded circuits too (QDC_RQ_PERM_SHARD)
   int rq_grad32 = 1;        // two-state passes hold up to FMAX_GRAD_RQ Gamma stages (QDC_RQ_GRAD32)
   int rq_maxcl = 1;         // relayouts chosen by max closure, else greedily (QDC_RQ_MAXCL)
   uint32_t rq_perm_low = 0;  // low positions a permuting pass fills, 0: default (QDC_RQ_PERM_LOW)
@@ -401,6 +402,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_SLOTS5")) rq_slots5 = atoi(e);
     if (const char* e = getenv("QDC_RQ_FWD5")) rq_fwd5 = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM")) rq_permute = atoi(e);
+    if (const char* e = getenv("QDC_RQ_PERM_SHARD")) rq_perm_shard = atoi(e);
     if (const char* e = getenv("QDC_RQ_GRAD32")) rq_grad32 = atoi(e);
     if (const char* e = getenv("QDC_RQ_MAXCL")) rq_maxcl = atoi(e);
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
@@ -855,8 +857,10 @@ struct Circuit {
   FusionPlanner planner() const {
     FusionPlanner P{ins, inexact, nl, fuse != 0, fuse_meas != 0, fuse_max_ops, fuse_lcmin};
     // gate-only passes permute their tile on the way out when they are register-resident
-    // (single-device layout only: the sharded remap planner owns the layout there)
-    P.permute = rq_permute && use_rq && g == 0 && sizeof(real) == 4;
+    // (sharded circuits too, round 5: later remaps' victims are relabelled, qdc_fusion.hpp
+    // relabel_remap; QDC_RQ_PERM_SHARD=0 keeps their layouts fixed)
+    P.permute = rq_permute && use_rq && (g == 0 || rq_perm_shard) && sizeof(real) == 4;
+    P.ng = g;
     P.rq_grad = rq_grad32 && use_rq && (sizeof(real) == 4 || rq64);
     if (rq_perm_low) P.perm_low = rq_perm_low;
     P.tile1_chunks = tile1_chunks;

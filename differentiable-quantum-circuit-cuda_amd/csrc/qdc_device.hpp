@@ -795,6 +795,29 @@ inline const char* pack(Ctx& c, const cx* src, cx* dst, const unsigned* victims,
   pg.lowc = (nl - g) - LV;
   pg.g = g;
   for (uint32_t k = 0; k < g; ++k) pg.vc[k] = victims[k] - LV;
+  // LDS tiles (k_pack_tile) whenever a tile fits the shard: every victim layout moves at
+  // streaming rates (QDC_PACK_TILE=0: the direct kernel)
+  static const bool tiled = [] {
+    const char* e = getenv("QDC_PACK_TILE");
+    return !(e && atoi(e) == 0);
+  }();
+  if (tiled && g <= 3 && pg.nchunks >= ((uint64_t)2 << PACK_KB) && pg.lowc >= PACK_KB) {
+    packtile pt{};
+    pt.nchunks = pg.nchunks;
+    pt.lowc = pg.lowc;
+    pt.g = g;
+    for (uint32_t k = 0; k < g; ++k) {
+      pt.vc[k] = pg.vc[k];
+      pt.nv += pg.vc[k] < PACK_KB ? 1u : 0u;
+    }
+    const uint32_t tgrid = (uint32_t)(pg.nchunks >> PACK_KB);
+    const char* cs = reinterpret_cast<const char*>(src);
+    if (unpack)
+      return c.launch("remap_unpack", 2.0 * state_bytes(nl), k_pack_tile<true>, tgrid,
+                      reinterpret_cast<const chunk*>(cs), reinterpret_cast<chunk*>(dst), pt);
+    return c.launch("remap_pack", 2.0 * state_bytes(nl), k_pack_tile<false>, tgrid,
+                    reinterpret_cast<const chunk*>(cs), reinterpret_cast<chunk*>(dst), pt);
+  }
   const uint32_t grid = (uint32_t)((pg.nchunks + BLOCK - 1) / BLOCK);
   if (unpack)
     return c.launch("remap_unpack", 2.0 * state_bytes(nl), k_pack<true>, grid,

@@ -87,6 +87,8 @@ struct FusionPlanner {
   // low physical positions a permuting pass fills with the qubits the next ops need first
   // (>= NLOW; more makes the next tiles' contiguous runs longer)
   uint32_t perm_low = (uint32_t)LV + 3;
+  // rank bits of a sharded circuit (permuting passes carry their permutation through remaps)
+  uint32_t ng = 0;
   // Mirrored schedules: the forward is scheduled so that its passes, run in reverse, are the
   // backward's passes (qdc_circuit.hpp mirror_schedule): on the two-state tile, under the
   // ordering rules of both directions, no gate after a density within a pass, and the
@@ -201,9 +203,16 @@ struct FusionPlanner {
     std::vector<uint32_t> free_low;  // low positions whose qubit is not wanted
     for (uint32_t p = 0; p < nlow; ++p)
       if (!ranked[p]) free_low.push_back(p);
+    // (sharded: positions < LV, inside the 16-B chunk, keep their qubit — a remap exchanges
+    // whole chunks, so a later remap's victim must never land there; the remap planner never
+    // picks them and remaps keep them in place)
     size_t f = 0;
-    for (uint32_t p : want)
-      if (p >= nlow) it.swaps.push_back({p, free_low[f++]});
+    for (uint32_t p : want) {
+      if (p < nlow) continue;
+      while (f < free_low.size() && ng > 0 && free_low[f] < (uint32_t)LV) ++f;
+      if (f == free_low.size()) break;
+      it.swaps.push_back({p, free_low[f++]});
+    }
     if (it.swaps.empty()) return;
     auto moved = [&](uint32_t p) {
       for (const auto& sw : it.swaps) {
@@ -216,10 +225,53 @@ struct FusionPlanner {
       plan[k].pos2 = moved(plan[k].pos2);
       plan[k].pos1 = moved(plan[k].pos1);
     }
+    // the rest of the plan: positions through the permutation; across a remap (sharded
+    // circuits) the permutation is carried through it (relabel_remap)
+    std::vector<uint32_t> pi(nl + ng);
+    for (uint32_t p = 0; p < nl + ng; ++p) pi[p] = p < nl ? moved(p) : p;
     for (size_t k = next; k < plan.size(); ++k) {
+      if (plan[k].type == QDC_PLAN_REMAP) {
+        relabel_remap(plan[k], pi);
+        continue;
+      }
       if (plan[k].type != QDC_PLAN_OP) continue;
-      plan[k].pos2 = moved(plan[k].pos2);
-      plan[k].pos1 = moved(plan[k].pos1);
+      plan[k].pos2 = pi[plan[k].pos2];
+      plan[k].pos1 = pi[plan[k].pos1];
+    }
+  }
+  // Sharded circuits (ng rank bits): the plan's positions assume the layout the remap planner
+  // simulated; a permuting pass changes the actual one by a permutation pi of the n physical
+  // positions (local to local, rank bits fixed at first).  A later remap must move the same
+  // logical qubits to the rank bits, so its victims become sorted(pi(V)); afterwards the actual
+  // layout differs from the planned one by pi' = M_{pi(V)} o pi o M_V^-1 (M_X: the layout
+  // change of a remap with victims X, qdc_shard.hpp QubitMap::apply), which may also reorder
+  // the rank bits — later remaps bring them back through the same formula.
+  void remap_map(const uint32_t* v, std::vector<uint32_t>& m) const {
+    const uint32_t L = nl, n = nl + ng;
+    m.assign(n, 0);
+    uint32_t c = 0;
+    for (uint32_t p = 0; p < L; ++p) {
+      bool vic = false;
+      for (uint32_t j = 0; j < ng; ++j) vic = vic || v[j] == p;
+      if (!vic) m[p] = c++;
+    }
+    for (uint32_t j = 0; j < ng; ++j) m[v[j]] = L + j;
+    for (uint32_t i = 0; i < ng; ++i) m[L + i] = L - ng + i;
+  }
+  void relabel_remap(qdc_plan_op& r, std::vector<uint32_t>& pi) const {
+    uint32_t nv[8];
+    for (uint32_t j = 0; j < ng; ++j) nv[j] = pi[r.victims[j]];
+    std::sort(nv, nv + ng);
+    std::vector<uint32_t> mv, mn, mvi(nl + ng), out(nl + ng);
+    remap_map(r.victims, mv);
+    remap_map(nv, mn);
+    for (uint32_t p = 0; p < nl + ng; ++p) mvi[mv[p]] = p;
+    for (uint32_t x = 0; x < nl + ng; ++x) out[x] = mn[pi[mvi[x]]];
+    pi.swap(out);
+    r.pack = 0;
+    for (uint32_t j = 0; j < ng; ++j) {
+      r.victims[j] = nv[j];
+      r.pack |= (nv[j] != nl - ng + j) ? 1 : 0;
     }
   }
 

@@ -336,15 +336,22 @@ inline bool spec_source_fp(const std::string& csrc, const std::string& inc, uint
 #ifndef QDC_RW_WAVES_HALF_ONE
 #define QDC_RW_WAVES_HALF_ONE 5
 #endif
+#ifndef QDC_PK_ASM  // (qdc_kernels.hpp; f64 builds never read them)
+#define QDC_PK_ASM 0
+#endif
+#ifndef QDC_PK_VASM
+#define QDC_PK_VASM 1
+#endif
 inline std::string spec_defines() {
   char b[512];
   snprintf(b, sizeof b,
            "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
            "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d "
-           "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d -DQDC_RW_WAVES_HALF_ONE=%d%s",
+           "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d -DQDC_RW_WAVES_HALF_ONE=%d -DQDC_PK_ASM=%d -DQDC_PK_VASM=%d "
+           "-DQDC_MATVEC_N=%d%s",
            (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
            (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE,
+           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE, (int)QDC_PK_ASM, (int)QDC_PK_VASM, (int)QDC_MATVEC_N,
            sizeof(real) == 8 ? " -DQDC_F64" : "");
   return b;
 }

@@ -720,6 +720,19 @@ __device__ __forceinline__ uint64_t fg_grab() {
 // two-qubit reverse step (A and B = 32 entries) and are re-read every iteration.
 #ifndef QDC_F64
 typedef float pk2 __attribute__((ext_vector_type(2)));
+// QDC_PK_ASM=1: each packed FMA as one inline-asm statement (rounds 1-4).  The hazard recognizer
+// pads inline asm conservatively — an s_nop 0 about every eighth packed FMA of a stage (r5:
+// ~1500 per two-state reverse program) — while for the same FMAs written with builtins it
+// knows the real latencies and pads none; the builtins fold the broadcast and swap into
+// op_sel / op_sel_hi and the negation into one SALU xor on the matrix entry's SGPR pair (dead
+// after its re halves: umatvec_n issues an entry's re halves before its im halves).
+#ifndef QDC_PK_ASM
+#define QDC_PK_ASM 0
+#endif
+#ifndef QDC_PK_VASM  // (QDC_PK_ASM=0: per-lane operands still as asm)
+#define QDC_PK_VASM 1
+#endif
+#if QDC_PK_ASM
 // one instruction per asm statement, so the scheduler can interleave independent chains
 __device__ __forceinline__ pk2 pk_re_fma(pk2 a, pk2 f, pk2 c) {  // c + a.re * (f.re, f.im)
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(c) : "s"(a), "v"(f));
@@ -735,6 +748,22 @@ __device__ __forceinline__ pk2 pk_re_mul(pk2 a, pk2 f) {  // a.re * (f.re, f.im)
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "s"(a), "v"(f));
   return r;
 }
+#else
+__device__ __forceinline__ pk2 pk_re_fma(pk2 a, pk2 f, pk2 c) {  // c + a.re * (f.re, f.im)
+  return __builtin_elementwise_fma(__builtin_shufflevector(a, a, 0, 0), f, c);
+}
+__device__ __forceinline__ pk2 pk_im_fma(pk2 a, pk2 f, pk2 c) {  // c + (-a.im f.im, a.im f.re)
+  const pk2 na = -a;
+  return __builtin_elementwise_fma(__builtin_shufflevector(na, a, 1, 3),
+                                   __builtin_shufflevector(f, f, 1, 0), c);
+}
+__device__ __forceinline__ pk2 pk_re_mul(pk2 a, pk2 f) {  // a.re * (f.re, f.im)
+  return __builtin_shufflevector(a, a, 0, 0) * f;
+}
+#endif
+#if QDC_PK_ASM || QDC_PK_VASM
+// per-lane operands (Gamma accumulation): inline asm, whose neg_lo modifier is free (the
+// builtins' (-b.im, b.im) pair costs a v_pk_add and two v_mov per use)
 __device__ __forceinline__ pk2 vpk_re_fma(pk2 a, pk2 f, pk2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(c) : "v"(a), "v"(f));
   return c;
@@ -744,6 +773,16 @@ __device__ __forceinline__ pk2 vpk_im_fma(pk2 a, pk2 f, pk2 c) {
       : "+v"(c) : "v"(a), "v"(f));
   return c;
 }
+__device__ __forceinline__ pk2 vpk_re_mul(pk2 a, pk2 f) {
+  pk2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(a), "v"(f));
+  return r;
+}
+#else
+__device__ __forceinline__ pk2 vpk_re_fma(pk2 a, pk2 f, pk2 c) { return pk_re_fma(a, f, c); }
+__device__ __forceinline__ pk2 vpk_im_fma(pk2 a, pk2 f, pk2 c) { return pk_im_fma(a, f, c); }
+__device__ __forceinline__ pk2 vpk_re_mul(pk2 a, pk2 f) { return pk_re_mul(a, f); }
+#endif
 __device__ __forceinline__ cx ucfma(cx a, cx f, cx c) {  // c + a f, a wave-uniform
   const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
   return __builtin_bit_cast(cx, pk_im_fma(A, F, pk_re_fma(A, F, __builtin_bit_cast(pk2, c))));
@@ -758,9 +797,7 @@ __device__ __forceinline__ cx vcfma(cx a, cx f, cx c) {  // c + a f, both per la
 }
 __device__ __forceinline__ cx vcmul(cx a, cx f) {  // a f, both per lane
   const pk2 A = __builtin_bit_cast(pk2, a), F = __builtin_bit_cast(pk2, f);
-  pk2 r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(A), "v"(F));
-  return __builtin_bit_cast(cx, vpk_im_fma(A, F, r));
+  return __builtin_bit_cast(cx, vpk_im_fma(A, F, vpk_re_mul(A, F)));
 }
 #else
 __device__ __forceinline__ cx ucfma(cx a, cx f, cx c) { return cfma(a, f, c); }
@@ -782,6 +819,42 @@ __device__ __forceinline__ void umatvec(const cx* M, cx (&x)[R]) {
   }
 #pragma unroll
   for (int p = 0; p < R; ++p) x[p] = y[p];
+}
+
+// NQ independent x <- M x at once, their dependency chains interleaved op by op.  A complex MAC
+// is two v_pk_fma_f32 on the same accumulator, and gfx950 wants 5 other VALU ops between a
+// packed FMA and the next one reading its result: one 4x4 matvec has only 4 chains (its outputs),
+// so on its own the compiler pads every round of them with an s_nop (r5: ~1500 per two-state
+// reverse pass program, 14 % of its VALU issue).  R * NQ >= 8 chains need none.
+template <int R, int NQ>
+__device__ __forceinline__ void umatvec_n(const cx* M, cx (&x)[NQ][R]) {
+#ifndef QDC_F64
+  // per column q: the re halves of every chain, then the im halves (R * NQ ops apart)
+  pk2 y[NQ][R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        const pk2 a = __builtin_bit_cast(pk2, M[p * R + q]), f = __builtin_bit_cast(pk2, x[n][q]);
+        y[n][p] = q == 0 ? pk_re_mul(a, f) : pk_re_fma(a, f, y[n][p]);
+      }
+#pragma unroll
+    for (int p = 0; p < R; ++p)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n)
+        y[n][p] = pk_im_fma(__builtin_bit_cast(pk2, M[p * R + q]), __builtin_bit_cast(pk2, x[n][q]),
+                            y[n][p]);
+  }
+#pragma unroll
+  for (int n = 0; n < NQ; ++n)
+#pragma unroll
+    for (int p = 0; p < R; ++p) x[n][p] = __builtin_bit_cast(cx, y[n][p]);
+#else
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) umatvec<R>(M, x[n]);
+#endif
 }
 
 // Lane select with a wave-uniform lane mask (v_cndmask): lanes set in `mask` take t.  Written
@@ -1286,6 +1359,71 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const chunk* __restrict__ src,
     stc(dst + idx, ldc(src + o));
   else
     stc(dst + o, ldc(src + idx));
+}
+#endif  // QDC_SPEC_TU
+
+// The same permutations through LDS tiles (round 5).  k_pack reads (UNPACK: writes) 16 B per
+// lane at victim-bit strides when a victim is a low chunk bit — and the remap planner's
+// farthest-next-use victims are often qubits 1..3 — so it moved a shard at 0.7-1.3 TB/s
+// (profiles/r5/r5c_shard_rehearsal.txt).  Here a block moves one tile of 2^KB chunks that is
+// contiguous in the unpacked index; its image in the packed index is 2^nv runs of 2^(KB - nv)
+// contiguous chunks (nv = victims below chunk bit KB <= 3), so both sides are whole-wave
+// accesses of >= 1 KiB.  Tile order s ("packed order"): the tile's non-victim bits compacted
+// low, its victim bits above them.
+struct packtile {
+  uint64_t nchunks;
+  uint32_t lowc, g, vc[8];  // as packgeo
+  uint32_t nv;              // victims below chunk bit PACK_KB (the first nv of vc)
+};
+constexpr uint32_t PACK_KB = 9;  // 512 chunks = 8 KiB of LDS per block
+#ifndef QDC_SPEC_TU
+template <bool UNPACK>
+__global__ __launch_bounds__(256) void k_pack_tile(const chunk* __restrict__ src,
+                                                   chunk* __restrict__ dst, packtile pg) {
+  __shared__ chunk lds[1u << PACK_KB];
+  const uint64_t base = (uint64_t)blockIdx.x << PACK_KB;  // tile base (unpacked index)
+  const uint32_t lowbits = PACK_KB - pg.nv;
+  auto remove_bit = [](uint64_t x, uint32_t b) {
+    return (x & ((1ull << b) - 1ull)) | ((x >> (b + 1)) << b);
+  };
+  // tile offset t (unpacked order) <-> packed order
+  auto ord = [&](uint32_t t) {
+    uint32_t hi = 0;
+    uint64_t x = t;
+    for (int k = (int)pg.nv - 1; k >= 0; --k) {
+      hi |= (uint32_t)((x >> pg.vc[k]) & 1ull) << k;
+      x = remove_bit(x, pg.vc[k]);
+    }
+    return (uint32_t)x | (hi << lowbits);
+  };
+  auto inv_ord = [&](uint32_t s) {
+    uint64_t x = s & ((1u << lowbits) - 1u);
+    for (uint32_t k = 0; k < pg.nv; ++k) x = insert_zero(x, pg.vc[k]);
+    for (uint32_t k = 0; k < pg.nv; ++k) x |= (uint64_t)((s >> (lowbits + k)) & 1u) << pg.vc[k];
+    return (uint32_t)x;
+  };
+  // packed index of unpacked chunk index i (the inverse of k_pack's expand)
+  auto packed = [&](uint64_t i) {
+    uint64_t j = 0;
+    for (int k = (int)pg.g - 1; k >= 0; --k) {
+      j |= ((i >> pg.vc[k]) & 1ull) << k;
+      i = remove_bit(i, pg.vc[k]);
+    }
+    return (j << pg.lowc) | i;
+  };
+  for (uint32_t s = threadIdx.x; s < (1u << PACK_KB); s += 256) {
+    if constexpr (UNPACK)
+      lds[s] = ldc(src + packed(base + inv_ord(s)));  // packed runs, in order
+    else
+      lds[ord(s)] = ldc(src + base + s);  // the contiguous unpacked tile
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < (1u << PACK_KB); s += 256) {
+    if constexpr (UNPACK)
+      stc(dst + base + s, lds[ord(s)]);
+    else
+      stc(dst + packed(base + inv_ord(s)), lds[s]);
+  }
 }
 #endif  // QDC_SPEC_TU
 

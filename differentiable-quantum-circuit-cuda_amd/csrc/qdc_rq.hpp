@@ -33,6 +33,11 @@ namespace qdc {
 #ifndef QDC_RQ_GSPLIT
 #define QDC_RQ_GSPLIT 0
 #endif
+// register stages apply their matrices to two quartets (four pairs) at once, the dependency
+// chains interleaved (umatvec_n); 0: one quartet (pair) at a time (rounds 1-4)
+#ifndef QDC_MATVEC_N
+#define QDC_MATVEC_N 1
+#endif
 
 constexpr int RQ_R = 16;  // amplitudes per thread per state
 constexpr uint32_t FK_RELAYOUT = 7;
@@ -114,29 +119,37 @@ __device__ __forceinline__ void rq_q2(cx (&f)[R], cx (&b)[R], const cx* __restri
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) A[i] = M[i];
-  // f with A, then b with B: one matrix (32 SGPRs) live at a time
+  // f with A, then b with B: one matrix (32 SGPRs) live at a time; two quartets at once (8
+  // interleaved dependency chains: no hazard padding between the packed FMAs, umatvec_n)
+  constexpr int NQ = (QDC_MATVEC_N && R / 4 >= 2) ? 2 : 1;
 #pragma unroll
-  for (int k = 0; k < R / 4; ++k) {
-    const int base = rq_base<S1, S2>(k);
-    cx x[4];
+  for (int k = 0; k < R / 4; k += NQ) {
+    cx x[NQ][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x[r] = f[rq_el<S1, S2>(base, r)];
-    umatvec<4>(A, x);
+    for (int n = 0; n < NQ; ++n)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) f[rq_el<S1, S2>(base, r)] = x[r];
+      for (int r = 0; r < 4; ++r) x[n][r] = f[rq_el<S1, S2>(rq_base<S1, S2>(k + n), r)];
+    umatvec_n<4, NQ>(A, x);
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f[rq_el<S1, S2>(rq_base<S1, S2>(k + n), r)] = x[n][r];
   }
   if constexpr (TWO) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) B[i] = M[16 + i];
 #pragma unroll
-    for (int k = 0; k < R / 4; ++k) {
-      const int base = rq_base<S1, S2>(k);
-      cx x[4];
+    for (int k = 0; k < R / 4; k += NQ) {
+      cx x[NQ][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[r] = b[rq_el<S1, S2>(base, r)];
-      umatvec<4>(B, x);
+      for (int n = 0; n < NQ; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) b[rq_el<S1, S2>(base, r)] = x[r];
+        for (int r = 0; r < 4; ++r) x[n][r] = b[rq_el<S1, S2>(rq_base<S1, S2>(k + n), r)];
+      umatvec_n<4, NQ>(B, x);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[rq_el<S1, S2>(rq_base<S1, S2>(k + n), r)] = x[n][r];
     }
   }
 }
@@ -215,18 +228,38 @@ __device__ __forceinline__ void rq_q1(cx (&f)[R], cx (&b)[R], const cx* __restri
     }
     wave_reduce_add<8>(v, acc_out);
   }
+  // four pairs at once (8 interleaved dependency chains, umatvec_n)
+  constexpr int NP = (QDC_MATVEC_N && R / 2 >= 4) ? 4 : 1;
 #pragma unroll
-  for (int k = 0; k < R / 2; ++k) {
-    const int j0 = ((k & ~LOWM) << 1) | (k & LOWM), j1 = j0 | (1 << S);
-    cx x[2] = {f[j0], f[j1]};
-    umatvec<2>(A, x);
-    f[j0] = x[0];
-    f[j1] = x[1];
+  for (int k = 0; k < R / 2; k += NP) {
+    cx x[NP][2];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      const int j0 = (((k + n) & ~LOWM) << 1) | ((k + n) & LOWM), j1 = j0 | (1 << S);
+      x[n][0] = f[j0];
+      x[n][1] = f[j1];
+    }
+    umatvec_n<2, NP>(A, x);
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      const int j0 = (((k + n) & ~LOWM) << 1) | ((k + n) & LOWM), j1 = j0 | (1 << S);
+      f[j0] = x[n][0];
+      f[j1] = x[n][1];
+    }
     if constexpr (TWO) {
-      cx y[2] = {b[j0], b[j1]};
-      umatvec<2>(B, y);
-      b[j0] = y[0];
-      b[j1] = y[1];
+#pragma unroll
+      for (int n = 0; n < NP; ++n) {
+        const int j0 = (((k + n) & ~LOWM) << 1) | ((k + n) & LOWM), j1 = j0 | (1 << S);
+        x[n][0] = b[j0];
+        x[n][1] = b[j1];
+      }
+      umatvec_n<2, NP>(B, x);
+#pragma unroll
+      for (int n = 0; n < NP; ++n) {
+        const int j0 = (((k + n) & ~LOWM) << 1) | ((k + n) & LOWM), j1 = j0 | (1 << S);
+        b[j0] = x[n][0];
+        b[j1] = x[n][1];
+      }
     }
   }
 }

@@ -284,6 +284,15 @@ const char* qdc_precompile(size_t qubits_number, int world, const int* kinds,
                            const qdc_complex* dens_grads, const size_t* dens_lens, size_t n_dens,
                            size_t* kernels);
 
+/* Test hook (host only): the runtime's forward schedule of `count` instructions over `world`
+ * shards, replayed against its layout: every op's positions where its logical qubits are,
+ * every remap's victims local and ascending (permuting passes relabel later remaps).  *items /
+ * *swaps (nullable): the schedule's items and permuting swaps.  Returns NULL, or the first
+ * inconsistency. */
+const char* qdc_check_schedule(size_t qubits_number, int world, const int* kinds,
+                               const unsigned* pos2, const unsigned* pos1, size_t count,
+                               size_t* items, size_t* swaps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -267,3 +267,51 @@ def test_specialized_passes_sharded(prec, kw):
         else:
             rel = np.linalg.norm(a2 - a0) / max(np.linalg.norm(a0), 1e-300)
             assert rel <= 1e-14, f"{kw}: specialized {name} differ by {rel:.2e}"
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_tiled_pack_equals_direct_pack(shards):
+    """The remap's pack / unpack through LDS tiles (k_pack_tile: whole-wave accesses whatever the
+    victims) is the same permutation as the direct kernel (k_pack): a deep random circuit whose
+    remaps pick low victims, on local shards, gives bit-identical densities, gradients and
+    states with QDC_PACK_TILE=0 and 1 (a process reads the knob once: two child processes)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    n = 18
+    code = f"""
+import sys, numpy as np
+sys.path[:0] = [{str(root)!r}, {str(root / 'differentiable-quantum-circuit-cuda_amd')!r}]
+import quantum_differentiable_circuit as q
+from quantum_differentiable_circuit import workloads as W
+ins, var = W.deep_random_circuit({n}, 600, seed=71)
+c = q.circuit_class("f32")({n}, local_shards={shards})
+for kind, pos in ins:
+    c._push(kind, *pos)
+vg = [np.ascontiguousarray(g, dtype=np.complex64) for g in var]
+d = c.forward([], vg)
+g = c.backward([np.diag([1.0, -1.0]).astype(np.complex64) for _ in d], [], vg)
+np.savez(sys.argv[1], d=np.concatenate([x.reshape(-1) for x in d]), g=np.concatenate(g),
+         f=c.get_state(0), b=c.get_state(2))
+"""
+    import tempfile
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for tile in ("0", "1"):
+            env = dict(os.environ, QDC_PACK_TILE=tile)
+            path = f"{td}/o{tile}.npz"
+            r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True,
+                               text=True, timeout=300)
+            assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+            z = np.load(path)
+            out[tile] = {k: z[k] for k in z.files}
+    for k in out["0"]:
+        assert np.array_equal(out["0"][k], out["1"][k]), f"{shards} shards: {k} differs"
+    ins, _ = __import__("quantum_differentiable_circuit.workloads", fromlist=["x"]).deep_random_circuit(n, 600, seed=71)
+    import quantum_differentiable_circuit as q
+    ops, _ = q.plan(n, shards, [(k, *p) for k, p in ins], 3, precision="f32")
+    low = [o["victims"] for o in ops if o["type"] == "remap" and o["pack"] and min(o["victims"]) < 10]
+    print(f"[pack] {shards} shards: {len(low)} remaps with victims below chunk bit 9; tiled == direct")
+    assert low, "the case must exercise low victims"

@@ -339,3 +339,41 @@ def test_rccl_id_file_rejects_stale(tmp_path):
     exchange_id(0, path, lambda: bytes(range(128)), start=now)
     t.join(timeout=30)
     assert got["raw"] == bytes(range(128))
+
+
+def _check_schedule(n, world, ins, precision="f32"):
+    import ctypes as C
+    from quantum_differentiable_circuit import _native
+    lib = _native.load(precision)
+    m = len(ins)
+    kinds = (C.c_int * m)(*[k for k, _ in ins])
+    a = (C.c_uint * m)(*[p[0] for _, p in ins])
+    b = (C.c_uint * m)(*[p[1] if len(p) > 1 else 0 for _, p in ins])
+    items, swaps = C.c_size_t(0), C.c_size_t(0)
+    err = lib.qdc_check_schedule(n, world, kinds, a, b, m, C.byref(items), C.byref(swaps))
+    assert not err, err.decode()
+    return items.value, swaps.value
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("case", ["layered", "brickwall", "random"])
+def test_permuting_passes_on_sharded_schedules(world, case, monkeypatch):
+    """Permuting passes on sharded circuits (qdc_fusion.hpp relabel_remap): replaying the layout
+    through the runtime's own forward schedule, every op finds its qubits where the plan puts
+    them and every remap's victims stay local and ascending; the permuting schedule needs fewer
+    items than fixed layouts (QDC_RQ_PERM_SHARD=0)."""
+    from quantum_differentiable_circuit import workloads as W
+    n = 22
+    if case == "layered":
+        ins, _ = W.layered_circuit(n, 6, 24)
+    elif case == "brickwall":
+        ins, _ = W.brickwall_circuit(n, 12, 30)
+    else:
+        ins, _ = W.deep_random_circuit(n, 1500, 33)
+    items, swaps = _check_schedule(n, world, ins)
+    monkeypatch.setenv("QDC_RQ_PERM_SHARD", "0")
+    items0, swaps0 = _check_schedule(n, world, ins)
+    print(f"[perm] {case} world={world}: {items} items ({swaps} swaps) vs {items0} fixed ({swaps0})")
+    if world > 1:
+        assert swaps0 == 0
+    assert swaps > 0 and items <= items0
