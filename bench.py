@@ -36,6 +36,32 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # vector peak (MI355X_MICROARCH.md; packed f32)
 
 
+class heartbeat:
+    """A progress line on stderr every `every` s while a long silent phase runs (the CPU
+    baseline's whole-step call takes minutes; a run that prints nothing for 3 minutes is taken
+    to be hung)."""
+
+    def __init__(self, label, every=30.0):
+        import threading
+        self.label, self.every, self.stop = label, every, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self.stop.wait(self.every):
+            print(f"[bench] {self.label}: {time.perf_counter() - t0:.0f} s", file=sys.stderr,
+                  flush=True)
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.t.join()
+        return False
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -610,10 +636,11 @@ def main():
             remaps = sum(o["type"] == "remap" for o in f_ops + b_ops)
 
     tw = time.perf_counter()
-    for _ in range(args.warmup):
-        c.forward([], vg)
-        c.backward(cots, [], vg)
-    c.synchronize()
+    with heartbeat("warm-up"):
+        for _ in range(args.warmup):
+            c.forward([], vg)
+            c.backward(cots, [], vg)
+        c.synchronize()
     # a program with more distinct specialized kernels than QDC_SPEC_MAX (C5's deep random
     # circuit) compiles them in the background while generic kernels run its passes: wait for
     # them (progress on stderr), then one more untimed step loads them
@@ -627,21 +654,23 @@ def main():
             if left == 0 or time.perf_counter() - tj > args.jit_wait_max_s:
                 break
         jit_bg_s = time.perf_counter() - tj
-        c.forward([], vg)
-        c.backward(cots, [], vg)
-        c.synchronize()
+        with heartbeat("warm-up on the specialized passes"):
+            c.forward([], vg)
+            c.backward(cots, [], vg)
+            c.synchronize()
     warmup_s = time.perf_counter() - tw  # includes the specialized kernels' compilation
 
     c.profile(True)
     c.host_times(reset=True)
     barrier(comm)
     c.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dens = c.forward([], vg)
-        grads = c.backward(cots, [], vg)
-    c.synchronize()
-    elapsed = time.perf_counter() - t0
+    with heartbeat("timed steps"):
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dens = c.forward([], vg)
+            grads = c.backward(cots, [], vg)
+        c.synchronize()
+        elapsed = time.perf_counter() - t0
     barrier(comm)
     stats = c.profile_collect()
     c.profile(False)
@@ -729,15 +758,17 @@ def main():
                 return fn(*a)
             except Exception as e:  # noqa: BLE001
                 return {"error": f"{type(e).__name__}: {e}"[:300]}
-        gate_kernels = aux(gate_kernel_sweep, args, n)
-        dense_kernels = aux(dense_gate_sample, args, n)
-        vqse = aux(vqse_sample)
-        abi = aux(abi_unfused_sample, args, n)
+        with heartbeat("auxiliary samples"):
+            gate_kernels = aux(gate_kernel_sweep, args, n)
+            dense_kernels = aux(dense_gate_sample, args, n)
+            vqse = aux(vqse_sample)
+            abi = aux(abi_unfused_sample, args, n)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args, args.cpu_qubits or n)
+            with heartbeat("CPU baseline (the reference's algorithm on the host cores)"):
+                cpu = cpu_baseline(args, args.cpu_qubits or n)
         except Exception as e:  # noqa: BLE001
             cpu = {"error": f"{type(e).__name__}: {e}"[:300]}
 
