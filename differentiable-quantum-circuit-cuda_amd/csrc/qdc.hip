@@ -509,6 +509,25 @@ QDC_API int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1,
   return 0;
 }
 
+// Host-only test hook of the LANE family's geometry (plan_lane): out[0..9] = {ampk + 1, nlow,
+// nf, f0, f1, m0, m1, units lo, units hi, it} for grid target 2048; reduces bit 1: the
+// block-wide variant (1024-chunk units).  Returns -1 on bad arguments, 1 when the state is too
+// small for the family.
+QDC_API int qdc_lane_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int reduces,
+                          unsigned* out) {
+  if (!out || (R != 2 && R != 4) || n < 2 || n > 62 || pos2 >= n || pos1 >= n ||
+      (R == 2 && pos2 != pos1) || (R == 4 && pos2 == pos1))
+    return -1;
+  qdc::Plan p;
+  if (!qdc::plan_lane(n, (int)R, pos2, pos1, 2048u, (reduces & 1) != 0, p, 1, (reduces & 2) ? 10u : 6u))
+    return 1;
+  const qdc::lgeo& g = p.lg;
+  const unsigned v[10] = {(unsigned)(p.ampk + 1), g.nlow, g.nf, g.f0, g.f1, g.m0, g.m1,
+                          (unsigned)(g.units & 0xffffffffu), (unsigned)(g.units >> 32), g.it};
+  for (int i = 0; i < 10; ++i) out[i] = v[i];
+  return 0;
+}
+
 // Host-only test hook of the specialized passes (qdc_jit.hpp): plan a pass over n stages (as
 // qdc_rq_plan; a two-state pass's stages all Gamma stages) on the runtime's tile of the
 // precision, write its kernel source and compile it with hipcc for gfx950 (not loaded).  name_out receives the kernel name

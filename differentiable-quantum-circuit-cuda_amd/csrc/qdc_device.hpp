@@ -148,11 +148,31 @@ struct Ctx {
   // one-state tile-family launches on 2^(10 + tile1_wide)-chunk tiles (1: K = 8, 32 KiB of LDS;
   // 2: K = 16, 64 KiB; knob QDC_TILE1_WIDE)
   uint32_t tile1_wide = 2;
+  // single-gate ops on the LANE family (k_lane: one chunk per lane, partners across lanes;
+  // knob QDC_LANE, one bit per op class: bit 0 reverse, bit 1 streaming one-state ops and
+  // injections, bit 2 densities and gradients).  Measured at n = 28 f32 (profiles/r5/
+  // r5k_*, r5l_*): apply 72-74 -> 76-84 % of 8 TB/s at most placements; the reverse with its
+  // gradient 77.5 -> 65-67 % at far targets (the tile family's 32 KiB runs per state win for
+  // two states), densities within +-1: bit 1 only
+  uint32_t lane_ops = 2;
+  // units in flight per wave of LANE launches, per class as lane_ops (knob QDC_LANE_U="u0,u1,u2";
+  // 1, 4 or 8)
+  uint32_t lane_u[3] = {8, 1, 4};
+  // chunks per state in flight per thread and step of the diagonal reverse kernels (knob
+  // QDC_DIAG_RU: 2 or 8; 8 = a block's step moves 32 KiB of each state, as the tile family):
+  // reverse_q2_diag 71.4 -> 73.3 % (profiles/r5/r5l_*)
+  uint32_t diag_ru = 8;
+  // streaming LANE launches with a target beyond the wave's chunk bits on the block-wide
+  // variant (k_lane_blk; knob QDC_LANE_BLK): +1..3.5 points at 13 of 27 far placements, -1..4
+  // at 5 (profiles/r5/r5m_*, r5n_*); the far-row cells that stay near 71 % (q1 20, 24) do so
+  // under every variant and block order tried: a DRAM-mapping effect of the row distance
+  // (tools/r5/stream_probe2.hip: plain two-row streams at chunk bit 20 reach 72.6 %)
+  uint32_t lane_blk = 1;
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
   cx* host_results = nullptr;  // pinned [FIN_MAX][RED]
-  std::vector<uint32_t> pending_dst;
+  std::vector<cx*> pending_dst;  // destinations (a slot of some reduction base)
   std::vector<uint32_t> pending_nb;
   cx* pending_base = nullptr;
   int pending_accumulate = 0;
@@ -184,6 +204,17 @@ struct Ctx {
     if (const char* e = getenv("QDC_XCD_MAP")) xcd_map = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE2_WIDE")) tile2_wide = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE1_WIDE")) tile1_wide = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_LANE")) lane_ops = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_DIAG_RU")) diag_ru = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_LANE_BLK")) lane_blk = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_LANE_U")) {
+      unsigned u0 = 0, u1 = 0, u2 = 0;
+      if (sscanf(e, "%u,%u,%u", &u0, &u1, &u2) == 3) {
+        lane_u[0] = u0;
+        lane_u[1] = u1;
+        lane_u[2] = u2;
+      }
+    }
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
@@ -340,9 +371,12 @@ struct Ctx {
 
   // --- reduction slots -----------------------------------------------------------------
   // A reduction kernel writes its per-block partials into the next free slot; the slot is
-  // later summed into base[dst*RED .. +RED) by k_finalize.  All pending slots share one base.
+  // later summed into base[dst*RED .. +RED) by k_finalize.  Pending slots may have different
+  // bases (the local shards of a circuit each reduce into their own buffers: one flush per
+  // shard launch was 8 finalize launches per pass at 8 shards, profiles/r5/r5c), not different
+  // accumulate modes.
   const char* begin_reduction(cx* base, int accumulate) {
-    if (base != pending_base || accumulate != pending_accumulate) QDC_TRY(flush());
+    if (accumulate != pending_accumulate) QDC_TRY(flush());
     pending_base = base;
     pending_accumulate = accumulate;
     if (pending_dst.size() == (size_t)FIN_MAX) QDC_TRY(flush());
@@ -351,7 +385,7 @@ struct Ctx {
   cx* slot_ptr() const { return partials + pending_dst.size() * (size_t)NBMAX * RED; }
   // nd: granule partials of a dynamic-tail pass in the slot's dparts row (0: none)
   void commit(uint32_t dst, uint32_t nb, uint32_t nd = 0) {
-    pending_dst.push_back(dst);
+    pending_dst.push_back(pending_base + (size_t)dst * RED);
     pending_nb.push_back(nb);
     pending_nd.push_back(nd);
   }
@@ -383,8 +417,8 @@ struct Ctx {
       }
       QDC_TRY(launch("finalize", 0.0, k_finalize,
                      (uint32_t)(j - i), (const cx*)(partials + i * (size_t)NBMAX * RED),
-                     (uint64_t)NBMAX * RED, pending_nb[i], tab, pending_base,
-                     pending_accumulate, p2, s2, n2));
+                     (uint64_t)NBMAX * RED, pending_nb[i], tab, pending_accumulate, p2, s2,
+                     n2));
       i = j;
     }
     pending_dst.clear();
@@ -399,10 +433,15 @@ struct Ctx {
 // ---------------------------------------------------------------------------------------
 struct Plan {
   bool tile = false;  // TILE family (a target at chunk bit 0..5) or DIRECT family
+  bool lane = false;  // LANE family (overrides both; k_lane)
   int R = 2;
   int mode = 0;       // DIRECT row layout (see rows<R, MODE>)
+  int ampk = -1;      // LANE: the gate bit held inside the chunk (f32 qubit 0), -1 none
+  int lu = 1;         // LANE: units in flight per wave (1, 4 or 8)
+  bool blk = false;   // LANE: the block-wide variant (k_lane_blk)
   geo g{};
   tgeo tg{};
+  lgeo lg{};
 };
 
 inline uint64_t nchunks_of(uint32_t n) { return ((uint64_t)1 << n) / VEC; }
@@ -498,6 +537,65 @@ inline Plan plan_gate(uint32_t n, int R, uint32_t pos2, uint32_t pos1, bool two_
   while (tpb * grid_target < p.tg.ntiles) tpb <<= 1;
   p.tg.tpb = (uint32_t)tpb;
   return p;
+}
+
+// LANE family geometry (k_lane): false when the state has fewer than 64 chunks.  Gate bit k
+// (0: pos1 / the q1 target, 1: pos2) is the in-chunk bit (f32 qubit 0) or a lane bit: chunk
+// bits below 6 - #far keep their own lane bit, the far ones take the top lane bits.
+// ub = 10: the block-wide variant (k_lane_blk, 1024-chunk units, partners through LDS).
+inline bool plan_lane(uint32_t n, int R, uint32_t pos2, uint32_t pos1, uint32_t grid_target,
+                      bool reduces, Plan& p, uint32_t lu = 1, uint32_t ub = 6) {
+  const uint64_t nch = nchunks_of(n);
+  if (nch < ((uint64_t)1 << ub)) return false;
+  const uint32_t pos[2] = {pos1, pos2};
+  const int nt = (R == 2) ? 1 : 2;
+  int ampk = -1;
+  uint32_t t[2] = {0, 0};
+  bool in_lane[2] = {false, false};
+  for (int k = 0; k < nt; ++k) {
+    if ((int)pos[k] < LV) {
+      ampk = k;
+    } else {
+      t[k] = pos[k] - LV;
+      in_lane[k] = true;
+    }
+  }
+  uint32_t nf = 0;
+  for (;;) {
+    uint32_t cnt = 0;
+    for (int k = 0; k < nt; ++k) cnt += (in_lane[k] && t[k] >= ub - nf) ? 1u : 0u;
+    if (cnt <= nf) break;
+    nf = cnt;
+  }
+  const uint32_t nlow = ub - nf;
+  uint32_t far[2] = {0, 0}, nfar = 0;
+  for (int k = 0; k < nt; ++k)
+    if (in_lane[k] && t[k] >= nlow) far[nfar++] = t[k];
+  if (nfar == 2 && far[0] > far[1]) std::swap(far[0], far[1]);
+  auto lane_bit = [&](uint32_t c) -> uint32_t {
+    if (c < nlow) return c;
+    return nlow + ((nfar == 2 && c == far[1]) ? 1u : 0u);
+  };
+  p = Plan{};
+  p.lane = true;
+  p.R = R;
+  p.ampk = ampk;
+  lgeo& g = p.lg;
+  g.units = nch >> ub;
+  p.blk = ub > 6;
+  g.nlow = nlow;
+  g.nf = nfar;
+  g.f0 = far[0];
+  g.f1 = far[1];
+  g.m0 = in_lane[0] ? (1u << lane_bit(t[0])) : 0u;
+  g.m1 = (nt == 2 && in_lane[1]) ? (1u << lane_bit(t[1])) : 0u;
+  // streaming: one step of lu units per wave; reductions: about grid_target blocks of 4 waves
+  p.lu = (lu >= 8) ? 8 : (lu >= 4) ? 4 : 1;
+  uint64_t it = (uint64_t)p.lu;
+  if (reduces)
+    while ((uint64_t)(BLOCK / 64) * it * grid_target < g.units) it <<= 1;
+  g.it = (uint32_t)it;
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -596,8 +694,28 @@ inline double state_bytes(uint32_t n) { return (double)((uint64_t)1 << n) * size
 constexpr int direct_u(int R) { return R == 2 ? 4 : 2; }
 
 inline uint32_t blocks_of(const Plan& p) {
+  if (p.lane && p.blk) return (uint32_t)p.lg.units;
+  if (p.lane) {
+    const uint64_t per = (uint64_t)(BLOCK / 64) * p.lg.it;
+    return (uint32_t)((p.lg.units + per - 1) / per);
+  }
   if (p.tile) return (uint32_t)((p.tg.ntiles + p.tg.tpb - 1) / p.tg.tpb);
   return (uint32_t)((p.g.items + (uint64_t)BLOCK * p.g.it - 1) / ((uint64_t)BLOCK * p.g.it));
+}
+
+template <int OP, int R, int U>
+inline const char* run_lane(Ctx& c, const char* name, double bytes, chunk* fc, chunk* bc,
+                            const mat<R>& A, const mat<R>& B, const Plan& p, uint32_t grid,
+                            cx* partials) {
+  if (p.ampk < 0)
+    return c.launch(name, bytes, k_lane<OP, R, -1, U>, grid, fc, bc, A, B, p.lg, partials);
+  if constexpr (VEC == 2) {
+    if (p.ampk == 0)
+      return c.launch(name, bytes, k_lane<OP, R, 0, U>, grid, fc, bc, A, B, p.lg, partials);
+    if constexpr (R == 4)
+      return c.launch(name, bytes, k_lane<OP, 4, 1, U>, grid, fc, bc, A, B, p.lg, partials);
+  }
+  return fail("invalid lane plan");
 }
 
 // Launch one gate-shaped op (any OP, R) on the family the plan selected.
@@ -607,6 +725,25 @@ inline const char* run_op(Ctx& c, const char* name, double bytes, cx* f, cx* b, 
   chunk* fc = reinterpret_cast<chunk*>(f);
   chunk* bc = reinterpret_cast<chunk*>(b);
   const uint32_t grid = blocks_of(p);
+  if (p.lane && p.blk) {
+    if constexpr (OP == OP_APPLY || OP == OP_INJECT || OP == OP_INJECT_FIRST) {
+      // 1024-thread blocks (one unit each)
+      if (p.ampk < 0)
+        return c.launch_block(name, bytes, k_lane_blk<OP, R, -1>, grid, (uint32_t)LB_NT, fc, bc, A, p.lg);
+      if constexpr (VEC == 2) {
+        if (p.ampk == 0)
+          return c.launch_block(name, bytes, k_lane_blk<OP, R, 0>, grid, (uint32_t)LB_NT, fc, bc, A, p.lg);
+        if constexpr (R == 4)
+          return c.launch_block(name, bytes, k_lane_blk<OP, 4, 1>, grid, (uint32_t)LB_NT, fc, bc, A, p.lg);
+      }
+    }
+    return fail("invalid block lane plan");
+  }
+  if (p.lane) {
+    if (p.lu == 8) return run_lane<OP, R, 8>(c, name, bytes, fc, bc, A, B, p, grid, partials);
+    if (p.lu == 4) return run_lane<OP, R, 4>(c, name, bytes, fc, bc, A, B, p, grid, partials);
+    return run_lane<OP, R, 1>(c, name, bytes, fc, bc, A, B, p, grid, partials);
+  }
   if (p.tile) {
     constexpr int K = op_two_states(OP) ? 2 : 4;
     if (K == 2 && p.tg.l + p.tg.h > 10)  // the widest two-state tile (QDC_TILE2_WIDE=2)
@@ -634,14 +771,24 @@ template <int R>
 inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, bool two,
                      bool reduces, bool writes_both = false) {
   const uint32_t cls = writes_both ? 0u : two ? 2u : 1u;  // QDC_TILE_FAR bit
-  Plan p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
-                     (c.tile_far >> cls) & 1u, c.tile2_wide, c.tile1_wide);
-  if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
+  Plan p;
+  const uint32_t lcls = writes_both ? 0u : reduces ? 2u : 1u;  // QDC_LANE bit
+  if (!((c.lane_ops >> lcls) & 1u) ||
+      !plan_lane(n, R, pos2, pos1, c.red_cap, reduces, p, c.lane_u[lcls])) {
+    p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
+                  (c.tile_far >> cls) & 1u, c.tile2_wide, c.tile1_wide);
+    if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
+  } else if (lcls == 1 && c.lane_blk && p.lg.nf > 0) {
+    // a far target: the block-wide variant, when the state holds a 1024-chunk unit
+    Plan q;
+    if (plan_lane(n, R, pos2, pos1, c.red_cap, reduces, q, 1, 10)) p = q;
+  }
   // XCD-aware order for streaming launches only by default: reductions (few long-lived blocks
   // with contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
-  p.g.xcd = p.tg.xcd = (c.xcd_map >> (reduces ? 1 : 0)) & 1u;  // bit 0 streaming, 1 reducing
+  p.g.xcd = p.tg.xcd = p.lg.xcd = (c.xcd_map >> (reduces ? 1 : 0)) & 1u;  // bit 0 streaming, 1 reducing
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
+  p.lg.gm = c.gm;
   return p;
 }
 
@@ -744,11 +891,17 @@ inline const char* reverse_diag(Ctx& c, cx* f, cx* b, const diag4& d, uint32_t p
   if (grad_base) {
     const dgeo g = diag_geo(c, n, pos2, pos1, c.red_cap);
     return reduce_into(c, grad_base, dst, 0, diag_blocks(g), [&](cx* out) {
+      if (c.diag_ru >= 8)
+        return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE_GRAD, 8>, diag_blocks(g),
+                        fc, bc, dc, d, g, out);
       return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE_GRAD, 2>, diag_blocks(g), fc,
                       bc, dc, d, g, out);
     });
   }
   const dgeo g = diag_geo(c, n, pos2, pos1, c.grid_cap);
+  if (c.diag_ru >= 8)
+    return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE, 8>, diag_blocks(g), fc, bc,
+                    dc, d, g, (cx*)nullptr);
   return c.launch("reverse_q2_diag", bytes, k_diag<DIAG_REVERSE, 2>, diag_blocks(g), fc, bc, dc,
                   d, g, (cx*)nullptr);
 }

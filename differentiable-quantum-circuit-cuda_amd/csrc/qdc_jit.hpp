@@ -337,7 +337,7 @@ inline bool spec_source_fp(const std::string& csrc, const std::string& inc, uint
 #define QDC_RW_WAVES_HALF_ONE 5
 #endif
 #ifndef QDC_PK_ASM  // (qdc_kernels.hpp; f64 builds never read them)
-#define QDC_PK_ASM 0
+#define QDC_PK_ASM 1
 #endif
 #ifndef QDC_PK_VASM
 #define QDC_PK_VASM 1
@@ -348,10 +348,10 @@ inline std::string spec_defines() {
            "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
            "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d "
            "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d -DQDC_RW_WAVES_HALF_ONE=%d -DQDC_PK_ASM=%d -DQDC_PK_VASM=%d "
-           "-DQDC_MATVEC_N=%d%s",
+           "-DQDC_MATVEC_N=%d -DQDC_RW_STAGGER=%d%s",
            (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
            (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE, (int)QDC_PK_ASM, (int)QDC_PK_VASM, (int)QDC_MATVEC_N,
+           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE, (int)QDC_PK_ASM, (int)QDC_PK_VASM, (int)QDC_MATVEC_N, (int)QDC_RW_STAGGER,
            sizeof(real) == 8 ? " -DQDC_F64" : "");
   return b;
 }

@@ -481,6 +481,331 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
 }
 
 // ---------------------------------------------------------------------------------------
+// LANE family (round 5): one 16-byte chunk per lane and state, the gate's partner
+// amplitudes fetched from other lanes of the wave.  A wave's "unit" is 64 chunks: its lanes
+// take the contiguous chunk bits 0..nlow-1 and the far targets' chunk bits as their top lane
+// bits (a q1 at chunk bit 20: lanes 0..31 read 32 consecutive chunks of row 0, lanes 32..63
+// the same chunks of row 1; targets below 6 - #far stay at their own lane bit).  Gate index
+// bit k (0: pos1 / the q1 target, 1: pos2) is either a lane bit (xor mask m_k, the partner
+// fetched with ds_bpermute) or, f32 only, the amplitude bit inside the chunk (qubit 0: AMPK).
+// Each lane computes the rows it holds, so the op's arithmetic is the minimum R complex MACs
+// per amplitude and matrix; the row a lane holds (rr) depends on its lane bits, so its
+// matrix coefficients are selected once per thread.  Measured motive (tools/r5/
+// stream_probe.hip): one chunk per lane in flight streams at 83-88 % of HBM, the direct rows'
+// R chunks per lane at 69-74 %.
+// ---------------------------------------------------------------------------------------
+struct lgeo {
+  uint64_t units;  // 64-chunk units of the state
+  uint32_t it;     // units per wave (block-contiguous iteration; reductions)
+  uint32_t nlow;   // contiguous low chunk bits of a unit (6 - nf)
+  uint32_t nf;     // far targets (0..2), lane bits nlow .. 5
+  uint32_t f0, f1; // their chunk bits, ascending
+  uint32_t m0, m1; // lane xor masks of gate bit 0 / 1 (0 for the in-chunk bit)
+  uint32_t xcd;    // XCD-aware block order (geo::xcd)
+  uint64_t gm;     // gap mask (geo::gm)
+};
+
+__device__ __forceinline__ uint64_t lane_chunk(const lgeo& g, uint64_t unit, uint32_t lane) {
+  uint64_t x = unit << g.nlow;
+  if (g.nf > 0) x = insert_zero(x, g.f0);
+  if (g.nf > 1) x = insert_zero(x, g.f1);
+  x |= lane & ((1u << g.nlow) - 1u);
+  if (g.nf > 0) x |= (uint64_t)((lane >> g.nlow) & 1u) << g.f0;
+  if (g.nf > 1) x |= (uint64_t)((lane >> (g.nlow + 1)) & 1u) << g.f1;
+  return x + (x & g.gm);
+}
+
+__device__ __forceinline__ real lane_xor(real v, uint32_t m) { return __shfl_xor(v, (int)m, 64); }
+__device__ __forceinline__ chunk chunk_xor(const chunk& c, uint32_t m) {
+  chunk r;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) r.v[v] = {lane_xor(c.v[v].x, m), lane_xor(c.v[v].y, m)};
+  return r;
+}
+
+// the chunks a lane needs: P[dl] = the chunk of lane ^ mask(dl), dl over the lane bits of d
+template <int R, int AMPK>
+struct lane_rows {
+  static constexpr uint32_t AMASK = AMPK >= 0 ? (1u << AMPK) : 0u;  // gate bit held in-chunk
+  static constexpr int NP = (R == 2) ? (AMPK >= 0 ? 1 : 2) : (AMPK >= 0 ? 2 : 4);
+  // P index of the lane part of a relative offset d
+  __device__ static constexpr int pidx(int d) {
+    const int dl = d & ~(int)AMASK;
+    if constexpr (R == 4 && AMPK == 0) return dl >> 1;
+    if constexpr (R == 4 && AMPK == 1) return dl;
+    return dl;
+  }
+  // xch(x, m): the chunk x of lane (thread) ^ m
+  template <class X>
+  __device__ static __forceinline__ void gather(const chunk& x, uint32_t m0, uint32_t m1, chunk (&P)[NP],
+                                                X&& xch) {
+    P[0] = x;
+    if constexpr (R == 2 && AMPK < 0) {
+      P[1] = xch(x, m0);
+    } else if constexpr (R == 4 && AMPK == 0) {
+      P[1] = xch(x, m1);
+    } else if constexpr (R == 4 && AMPK == 1) {
+      P[1] = xch(x, m0);
+    } else if constexpr (R == 4) {
+      P[1] = xch(x, m0);
+      P[2] = xch(x, m1);
+      P[3] = xch(x, m0 | m1);
+    }
+  }
+  __device__ static __forceinline__ void gather(const chunk& x, uint32_t m0, uint32_t m1, chunk (&P)[NP]) {
+    gather(x, m0, m1, P, [](const chunk& c, uint32_t m) { return chunk_xor(c, m); });
+  }
+  // out.v[v] = sum_d cf[v][d] * (amplitude at offset d from v's row)
+  __device__ static __forceinline__ void rows_out(const cx (&cf)[VEC][R], const chunk (&P)[NP], chunk& out) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      cx y = cmul(cf[v][0], at(P, v, 0));
+#pragma unroll
+      for (int d = 1; d < R; ++d) y = cfma(cf[v][d], at(P, v, d), y);
+      out.v[v] = y;
+    }
+  }
+  // the amplitude at relative row offset d from amplitude v's own row
+  __device__ static __forceinline__ cx at(const chunk (&P)[NP], int v, int d) {
+    const int vf = AMPK >= 0 ? (v ^ ((d >> (AMPK < 0 ? 0 : AMPK)) & 1)) : v;
+    return P[pidx(d)].v[vf];
+  }
+  // own row of amplitude v: the lane bits' part rl (runtime) and the in-chunk bit (v)
+  __device__ static constexpr uint32_t amp_part(int v) { return AMPK >= 0 ? ((uint32_t)v << AMPK) : 0u; }
+};
+
+// coefficient M[rr][rr ^ d] for rr = rl | amp_part(v), selected over the lane part rl
+template <int R, int AMPK>
+__device__ __forceinline__ cx lane_coef(const mat<R>& M, uint32_t rl, int v, int d) {
+  using L = lane_rows<R, AMPK>;
+  const uint32_t av = L::amp_part(v);
+  cx c = M.a[av * R + (av ^ (uint32_t)d)];
+#pragma unroll
+  for (uint32_t r = 1; r < (uint32_t)R; ++r) {
+    if (r & L::AMASK) continue;
+    const uint32_t rr = r | av;
+    const cx cr = M.a[rr * R + (rr ^ (uint32_t)d)];
+    c.x = (rl == r) ? cr.x : c.x;
+    c.y = (rl == r) ? cr.y : c.y;
+  }
+  return c;
+}
+
+template <int OP, int R, int AMPK, int U>
+__global__ __launch_bounds__(BLOCK) void k_lane(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                mat<R> A, mat<R> B, lgeo g,
+                                                cx* __restrict__ partials) {
+  using L = lane_rows<R, AMPK>;
+  constexpr int NP = L::NP;
+  constexpr bool RD = op_reduces(OP);
+  // accumulators per relative offset, and per in-chunk amplitude when that bit is a gate bit
+  // (else both amplitudes of a chunk share the row and one accumulator set)
+  constexpr int NV = AMPK >= 0 ? VEC : 1;
+  constexpr int NACC = RD ? NV * R : 1;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the lane part of this lane's row index
+  uint32_t rl = 0;
+  if (AMPK != 0) rl |= (lane & g.m0) ? 1u : 0u;
+  if (R == 4 && AMPK != 1) rl |= (lane & g.m1) ? 2u : 0u;
+  // coefficients of the matrices this op applies, per own amplitude and relative offset
+  constexpr bool USE_A = OP == OP_APPLY || OP == OP_REVERSE || OP == OP_REVERSE_GRAD ||
+                         OP == OP_INJECT || OP == OP_INJECT_FIRST;
+  constexpr bool USE_B = OP == OP_REVERSE || OP == OP_REVERSE_GRAD;
+  cx ca[USE_A ? VEC : 1][R], cb[USE_B ? VEC : 1][R];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+      if constexpr (USE_A) ca[v][d] = lane_coef<R, AMPK>(A, rl, v, d);
+      if constexpr (USE_B) cb[v][d] = lane_coef<R, AMPK>(B, rl, v, d);
+    }
+  cx acc[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) acc[k] = {0, 0};
+  const uint64_t blk = xcd_block(blockIdx.x, gridDim.x, g.xcd);
+  // U units per wave in flight: every load of a step is issued before its first exchange;
+  // a block's step covers 4U consecutive units.  Blocks whose units all exist run unguarded.
+  auto body = [&](auto guarded) __attribute__((always_inline)) {
+  for (uint32_t s = 0; s < g.it; s += U) {
+    uint64_t cc[U];
+    chunk fxs[U], bxs[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t unit = (blk * g.it + s + u) * (BLOCK / 64) + wave;
+      ok[u] = !decltype(guarded)::value || unit < g.units;  // wave-uniform
+      cc[u] = lane_chunk(g, ok[u] ? unit : 0, lane);
+      if (ok[u]) {
+        fxs[u] = ldc(f + cc[u]);
+        if constexpr (op_reads_b(OP)) bxs[u] = ldc(b + cc[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const uint64_t c = cc[u];
+      chunk fx = fxs[u], bx = bxs[u];
+      if constexpr (OP == OP_APPLY) {
+        chunk P[NP];
+        L::gather(fx, g.m0, g.m1, P);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          cx y = cmul(ca[v][0], L::at(P, v, 0));
+#pragma unroll
+          for (int d = 1; d < R; ++d) y = cfma(ca[v][d], L::at(P, v, d), y);
+          fx.v[v] = y;
+        }
+        stc(f + c, fx);
+      } else if constexpr (OP == OP_REVERSE || OP == OP_REVERSE_GRAD) {
+        chunk P[NP], Q[NP];
+        L::gather(fx, g.m0, g.m1, P);
+        L::gather(bx, g.m0, g.m1, Q);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          cx y = cmul(ca[v][0], L::at(P, v, 0));
+#pragma unroll
+          for (int d = 1; d < R; ++d) y = cfma(ca[v][d], L::at(P, v, d), y);
+          fx.v[v] = y;  // uncomputed own amplitude
+          if constexpr (OP == OP_REVERSE_GRAD) {
+#pragma unroll
+            for (int d = 0; d < R; ++d)
+              acc[(AMPK >= 0 ? v : 0) * R + d] = cfma(L::at(Q, v, d), y, acc[(AMPK >= 0 ? v : 0) * R + d]);
+          }
+          cx z = cmul(cb[v][0], L::at(Q, v, 0));
+#pragma unroll
+          for (int d = 1; d < R; ++d) z = cfma(cb[v][d], L::at(Q, v, d), z);
+          bx.v[v] = z;
+        }
+        stc(f + c, fx);
+        stc(b + c, bx);
+      } else if constexpr (OP == OP_INJECT || OP == OP_INJECT_FIRST) {
+        chunk t;
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) t.v[v] = {2 * fx.v[v].x, -2 * fx.v[v].y};
+        chunk P[NP];
+        L::gather(t, g.m0, g.m1, P);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          cx y = cmul(ca[v][0], L::at(P, v, 0));
+#pragma unroll
+          for (int d = 1; d < R; ++d) y = cfma(ca[v][d], L::at(P, v, d), y);
+          bx.v[v] = (OP == OP_INJECT) ? cadd(bx.v[v], y) : y;
+        }
+        stc(b + c, bx);
+      } else if constexpr (OP == OP_DENSITY) {
+        chunk P[NP];
+        L::gather(fx, g.m0, g.m1, P);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+#pragma unroll
+          for (int d = 0; d < R; ++d) acc[(AMPK >= 0 ? v : 0) * R + d] =
+              cfma_conj(fx.v[v], L::at(P, v, d), acc[(AMPK >= 0 ? v : 0) * R + d]);
+      } else {  // OP_GRAD
+        chunk P[NP];
+        L::gather(fx, g.m0, g.m1, P);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+#pragma unroll
+          for (int d = 0; d < R; ++d) acc[(AMPK >= 0 ? v : 0) * R + d] =
+              cfma(bx.v[v], L::at(P, v, d), acc[(AMPK >= 0 ? v : 0) * R + d]);
+      }
+    }
+  }
+  };
+  if ((blk + 1) * g.it * (BLOCK / 64) <= g.units)
+    body(std::false_type{});
+  else
+    body(std::true_type{});
+  if constexpr (RD) {
+    // sum over the lanes that share a row index (the lane bits outside the gate's masks),
+    // then one lane per row class stores its VEC*R sums at their absolute (p, q) slots
+    __shared__ cx red[BLOCK / 64][R * R];
+    const uint32_t tm = g.m0 | g.m1;
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+      real x = acc[k].x, y = acc[k].y;
+#pragma unroll
+      for (uint32_t o = 32; o > 0; o >>= 1) {
+        if (tm & o) continue;  // uniform
+        x += __shfl_xor(x, (int)o, 64);
+        y += __shfl_xor(y, (int)o, 64);
+      }
+      acc[k] = {x, y};
+    }
+    if ((lane & ~tm) == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const uint32_t rr = rl | L::amp_part(v);
+#pragma unroll
+        for (int d = 0; d < R; ++d) {
+          // REVERSE_GRAD: p from b (offset), q = own uncomputed f; others: p own, q offset
+          const uint32_t idx = (OP == OP_REVERSE_GRAD) ? ((rr ^ (uint32_t)d) * R + rr)
+                                                       : (rr * R + (rr ^ (uint32_t)d));
+          red[wave][idx] = acc[v * R + d];
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t < RED) {
+      cx s = {0, 0};
+      if (t < R * R) {
+        s = red[0][t];
+#pragma unroll
+        for (int w = 1; w < BLOCK / 64; ++w) s = cadd(s, red[w][t]);
+      }
+      partials[(uint64_t)blockIdx.x * RED + t] = s;
+    }
+  }
+}
+
+// Block-wide LANE variant for streaming one-state ops and injections (QDC_LANE_BLK): a unit is
+// 1024 chunks, one per thread of a 1024-thread block; far targets take the top thread bits, so
+// every wave instruction moves one contiguous KiB and a block reads runs of 1024 / R chunks of
+// each row; partners come through LDS (16 KiB, one barrier).  Measured motive (tools/r5/
+// stream_probe2.hip): at far row bits where the DRAM mapping makes two 512-B streams per wave
+// slow (row bit 20: 72.6 %), 8 KiB runs per row and block stream at 77 %.
+constexpr int LB_NT = 1024;
+template <int OP, int R, int AMPK>
+__global__ __launch_bounds__(LB_NT) void k_lane_blk(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                    mat<R> A, lgeo g) {
+  static_assert(OP == OP_APPLY || OP == OP_INJECT || OP == OP_INJECT_FIRST, "streaming ops");
+  using L = lane_rows<R, AMPK>;
+  __shared__ chunk lds[LB_NT];
+  const uint32_t t = threadIdx.x;
+  uint32_t rl = 0;
+  if (AMPK != 0) rl |= (t & g.m0) ? 1u : 0u;
+  if (R == 4 && AMPK != 1) rl |= (t & g.m1) ? 2u : 0u;
+  cx ca[VEC][R];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int d = 0; d < R; ++d) ca[v][d] = lane_coef<R, AMPK>(A, rl, v, d);
+  const uint64_t unit = xcd_block(blockIdx.x, gridDim.x, g.xcd);
+  const uint64_t c = lane_chunk(g, unit, t);
+  chunk x = ldc(f + c), bx;
+  if constexpr (OP == OP_INJECT) bx = ldc(b + c);
+  if constexpr (OP != OP_APPLY) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) x.v[v] = {2 * x.v[v].x, -2 * x.v[v].y};
+  }
+  lds[t] = x;
+  __syncthreads();
+  chunk P[L::NP], y;
+  L::gather(x, g.m0, g.m1, P, [&](const chunk&, uint32_t m) { return lds[t ^ m]; });
+  L::rows_out(ca, P, y);
+  if constexpr (OP == OP_APPLY) {
+    stc(f + c, y);
+  } else {
+    if constexpr (OP == OP_INJECT) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) y.v[v] = cadd(bx.v[v], y.v[v]);
+    }
+    stc(b + c, y);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Diagonal two-qubit gates: purely elementwise over chunks, every position pair is a fully
 // contiguous stream.  k = 2 bit(i,pos2) + bit(i,pos1)  (primitives.cu:649-672, 398-452).
 //   DIAG_APPLY: s <- d s;  DIAG_REVERSE[_GRAD]: f <- dc f; [G[k] += b f]; b <- d b;
@@ -565,8 +890,8 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
 // dst[slot_dst[s]*RED + k] (+)= sum_b partials[s][b][k].
 // ---------------------------------------------------------------------------------------
 constexpr int FIN_MAX = 32;
-struct fin_table {
-  uint32_t dst[FIN_MAX];
+struct fin_table {  // each slot's destination (its reduction base + slot index, resolved)
+  cx* dst[FIN_MAX];
 };
 
 // Granule partials of a dynamic-tail pass, pre-summed: block (slot y, chunk x) adds the BLOCK
@@ -589,8 +914,7 @@ __global__ __launch_bounds__(BLOCK) void k_dsum(const cx* __restrict__ parts, ui
 #ifndef QDC_SPEC_TU  // (not in the specialized kernels' translation units)
 __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ partials,
                                                     uint64_t slot_stride, uint32_t nblocks,
-                                                    fin_table tab, cx* __restrict__ dst,
-                                                    int accumulate, const cx* __restrict__ partials2,
+                                                    fin_table tab, int accumulate, const cx* __restrict__ partials2,
                                                     uint64_t slot_stride2, uint32_t n2) {
   const cx* p = partials + (uint64_t)blockIdx.x * slot_stride;
   const cx* p2 = partials2 + (uint64_t)blockIdx.x * slot_stride2;
@@ -606,7 +930,7 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(const cx* __restrict__ parti
   block_reduce_store<RED>(acc, out);
   __syncthreads();
   if (threadIdx.x < RED) {
-    cx* d = dst + (uint64_t)tab.dst[blockIdx.x] * RED + threadIdx.x;
+    cx* d = tab.dst[blockIdx.x] + threadIdx.x;
     *d = accumulate ? cadd(*d, out[threadIdx.x]) : out[threadIdx.x];
   }
 }
@@ -720,14 +1044,17 @@ __device__ __forceinline__ uint64_t fg_grab() {
 // two-qubit reverse step (A and B = 32 entries) and are re-read every iteration.
 #ifndef QDC_F64
 typedef float pk2 __attribute__((ext_vector_type(2)));
-// QDC_PK_ASM=1: each packed FMA as one inline-asm statement (rounds 1-4).  The hazard recognizer
+// QDC_PK_ASM=1 (default): each packed FMA as one inline-asm statement.  The hazard recognizer
 // pads inline asm conservatively — an s_nop 0 about every eighth packed FMA of a stage (r5:
-// ~1500 per two-state reverse program) — while for the same FMAs written with builtins it
-// knows the real latencies and pads none; the builtins fold the broadcast and swap into
-// op_sel / op_sel_hi and the negation into one SALU xor on the matrix entry's SGPR pair (dead
-// after its re halves: umatvec_n issues an entry's re halves before its im halves).
+// ~1000-1500 per two-state reverse program) — while for the same FMAs written with builtins
+// (QDC_PK_ASM=0) it pads none: those fold the broadcast and swap into op_sel / op_sel_hi and the
+// negation into a SALU xor on the matrix entry's SGPR pair (QDC_PK_VASM=0: per-lane operands
+// too, where the (-b.im, b.im) pair costs a v_pk_add and two v_mov).  Measured same box,
+// bit-identical outputs (profiles/r5/r5d_pk_forms_ab.txt, C2 n = 28): asm 4660-4668 gates/s,
+// builtins for the matrix operands 4572-4585, builtins throughout 4354 — the pads cost nothing
+// with two waves per SIMD (the partner wave issues in their cycles), the SALU xors and moves do.
 #ifndef QDC_PK_ASM
-#define QDC_PK_ASM 0
+#define QDC_PK_ASM 1
 #endif
 #ifndef QDC_PK_VASM  // (QDC_PK_ASM=0: per-lane operands still as asm)
 #define QDC_PK_VASM 1

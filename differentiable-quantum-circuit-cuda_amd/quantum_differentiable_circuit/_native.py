@@ -34,7 +34,7 @@ RUNTIME = (
     "qdc_comm_free", "qdc_comm_allreduce", "qdc_circuit_gather_state", "qdc_circuit_new_sharded", "qdc_circuit_new_local_shards",
     "qdc_circuit_new_devices",
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
-    "qdc_rq_plan", "qdc_spec_selftest", "qdc_gate_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
+    "qdc_rq_plan", "qdc_spec_selftest", "qdc_gate_plan", "qdc_lane_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
     "qdc_jit_stats", "qdc_jit_dir", "qdc_spec_fingerprint", "qdc_spec_selftest_batch",
     "qdc_jit_wait", "qdc_precompile", "qdc_check_schedule",
 )
@@ -121,6 +121,8 @@ def _proto(lib):
         "qdc_abi_profile": (_E, [C.c_int]),
         "qdc_abi_profile_collect": (_S, [C.POINTER(KernelStat), _S]),
         "qdc_gate_plan": (C.c_int, [C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int,
+                                    C.POINTER(C.c_uint)]),
+        "qdc_lane_plan": (C.c_int, [C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_int,
                                     C.POINTER(C.c_uint)]),
         "qdc_spec_selftest": (C.c_char_p, [C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                                            C.POINTER(C.c_uint), C.POINTER(C.c_ulonglong), _S,

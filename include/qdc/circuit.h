@@ -246,6 +246,16 @@ const char* qdc_spec_selftest_batch(unsigned tile_bits, const size_t* counts, si
 int qdc_gate_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int two_states,
                   int far_tile, unsigned* out);
 
+/* Test hook (host only): the LANE family's geometry (qdc_device.hpp plan_lane; one chunk per
+ * lane, partner amplitudes across lanes).  out[0..9] = {in-chunk gate bit + 1 (0: none),
+ * contiguous low chunk bits of a 64-chunk unit, far targets, their chunk bits f0 and f1,
+ * lane masks of gate bits 0 (pos1) and 1 (pos2), units low 32 bits, high 32 bits, units per
+ * wave (reduces bit 0: a grid of about 2048 blocks)}; reduces bit 1: the block-wide variant
+ * (k_lane_blk: 1024-chunk units, thread masks).  Returns 0, 1 when the state has fewer chunks
+ * than a unit, -1 on invalid arguments. */
+int qdc_lane_plan(unsigned n, unsigned R, unsigned pos2, unsigned pos1, int reduces,
+                  unsigned* out);
+
 /* The specialized-kernel cache of this process (qdc_jit.hpp).  stats[0..8] (up to n) =
  * {kernels compiled by this process, kernels waited for while another process compiled them,
  * (kernel, device) loads, seconds compiling, seconds waiting, seconds in the cache overall

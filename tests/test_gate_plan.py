@@ -106,3 +106,136 @@ def test_gate_plan_rejects_invalid_arguments():
     assert lib.qdc_gate_plan(10, 2, 2, 1, 0, 0, out) == -1   # q1 with two positions
     assert lib.qdc_gate_plan(10, 4, 3, 3, 0, 0, out) == -1   # q2 on one qubit
     assert lib.qdc_gate_plan(10, 2, 10, 10, 0, 0, out) == -1  # position out of range
+
+
+# ---------------------------------------------------------------------------------------
+# LANE family (k_lane, csrc/qdc_kernels.hpp): one chunk per lane, partners across lanes.
+# ---------------------------------------------------------------------------------------
+def lane_plan(prec, n, R, pos2, pos1, reduces=False, blk=False):
+    lib = load(prec)
+    out = (C.c_uint * 10)()
+    rc = lib.qdc_lane_plan(n, R, pos2, pos1, int(reduces) | (2 if blk else 0), out)
+    if rc == 1:
+        return None
+    assert rc == 0
+    keys = ("ampk1", "nlow", "nf", "f0", "f1", "m0", "m1", "lo", "hi", "it")
+    d = dict(zip(keys, list(out)))
+    d["units"] = d["lo"] | (d["hi"] << 32)
+    d["ampk"] = d["ampk1"] - 1
+    d["ub"] = 10 if blk else 6
+    return d
+
+
+def lane_chunks(p):
+    """lane_chunk(g, unit, lane) for every unit and lane: (units, 2^ub) chunk indices."""
+    u = np.arange(p["units"], dtype=np.int64)[:, None]
+    lane = np.arange(1 << p["ub"], dtype=np.int64)[None, :]
+    x = u << p["nlow"]
+    if p["nf"] > 0:
+        x = insert_zero(x, p["f0"])
+    if p["nf"] > 1:
+        x = insert_zero(x, p["f1"])
+    x = x | (lane & ((1 << p["nlow"]) - 1))
+    if p["nf"] > 0:
+        x = x | (((lane >> p["nlow"]) & 1) << p["f0"])
+    if p["nf"] > 1:
+        x = x | (((lane >> (p["nlow"] + 1)) & 1) << p["f1"])
+    return x
+
+
+def lane_emulate(p, R, M, psi, vec):
+    """k_lane's arithmetic restated: every lane holds its chunk, gathers the chunks of lanes
+    lane ^ mask(d) and computes its own rows with the coefficients M[rr][rr ^ d]; also the
+    density accumulators at their absolute (rr, rr ^ d) slots.  Returns (M psi, rho)."""
+    ch = lane_chunks(p)
+    amps = psi.reshape(-1, vec)[ch]                     # (units, 2^ub, vec)
+    lane = np.arange(1 << p["ub"])
+    ampk, m0, m1 = p["ampk"], p["m0"], p["m1"]
+    rl = np.zeros(lane.size, np.int64)
+    if ampk != 0:
+        rl |= ((lane & m0) != 0).astype(np.int64)
+    if R == 4 and ampk != 1:
+        rl |= ((lane & m1) != 0).astype(np.int64) << 1
+    out = np.zeros_like(amps)
+    rho = np.zeros((R, R), dtype=psi.dtype)
+    for v in range(vec):
+        rr = rl | ((v << ampk) if ampk >= 0 else 0)
+        y = 0
+        for d in range(R):
+            lm = (m0 if (d & 1) and ampk != 0 else 0) | (m1 if (d & 2) and ampk != 1 else 0)
+            vf = v ^ ((d >> ampk) & 1) if ampk >= 0 else v
+            partner = amps[:, lane ^ lm, vf]
+            y = y + M[rr, rr ^ d][None, :] * partner
+            contrib = (amps[:, :, v] * np.conj(partner)).sum(axis=0)
+            np.add.at(rho, (rr, rr ^ d), contrib)
+        out[:, :, v] = y
+    res = psi.copy().reshape(-1, vec)
+    res[ch] = out
+    return res.reshape(-1), rho
+
+
+def gate_reference(R, M, psi, n, pos2, pos1):
+    i = np.arange(1 << n)
+    if R == 2:
+        b = (i >> pos1) & 1
+        i0 = i & ~(1 << pos1)
+        return M[b, 0] * psi[i0] + M[b, 1] * psi[i0 | (1 << pos1)]
+    r = ((i >> pos2) & 1) * 2 + ((i >> pos1) & 1)
+    base = i & ~((1 << pos2) | (1 << pos1))
+    out = 0
+    for qq in range(4):
+        j = base | (((qq >> 1) & 1) << pos2) | ((qq & 1) << pos1)
+        out = out + M[r, qq] * psi[j]
+    return out
+
+
+def density_reference(R, psi, n, pos2, pos1):
+    i = np.arange(1 << n)
+    r = ((i >> pos1) & 1) if R == 2 else ((i >> pos2) & 1) * 2 + ((i >> pos1) & 1)
+    rho = np.zeros((R, R), dtype=psi.dtype)
+    base = i & ~((1 << pos2) | (1 << pos1))
+    sel = base == i
+    for a in range(R):
+        for b in range(R):
+            ja = base | (((a >> 1) & 1) << pos2 if R == 4 else 0) | ((a & 1) << pos1)
+            jb = base | (((b >> 1) & 1) << pos2 if R == 4 else 0) | ((b & 1) << pos1)
+            rho[a, b] = (psi[ja[sel]] * np.conj(psi[jb[sel]])).sum()
+    return rho
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("n,blk", [(7, False), (9, False), (12, False), (11, True), (14, True)])
+def test_lane_geometry_covers_state_and_applies_gate(prec, n, blk):
+    lv = 1 if prec == "f32" else 0
+    vec = 1 << lv
+    ub = 10 if blk else 6
+    rng = np.random.default_rng(n)
+    psi = rng.standard_normal(1 << n) + 1j * rng.standard_normal(1 << n)
+    for R, pos2, pos1 in cases(n):
+        p = lane_plan(prec, n, R, pos2, pos1, blk=blk)
+        if (1 << n) // vec < (1 << ub):
+            assert p is None
+            continue
+        assert p is not None and p["units"] == (1 << (n - lv)) >> ub
+        assert p["nlow"] + p["nf"] == ub and (p["nf"] < 2 or p["f0"] < p["f1"])
+        ch = lane_chunks(p)
+        seen = np.zeros(1 << (n - lv), np.int32)
+        np.add.at(seen, ch.reshape(-1), 1)
+        assert (seen == 1).all(), (prec, n, R, pos2, pos1, p)
+        M = rng.standard_normal((R, R)) + 1j * rng.standard_normal((R, R))
+        got, rho = lane_emulate(p, R, M, psi, vec)
+        want = gate_reference(R, M, psi, n, pos2, pos1)
+        assert np.allclose(got, want, atol=1e-12), (prec, n, R, pos2, pos1, p)
+        assert np.allclose(rho, density_reference(R, psi, n, pos2, pos1), atol=1e-9), \
+            (prec, n, R, pos2, pos1, p)
+
+
+def test_lane_plan_reduction_grid_and_invalid_arguments():
+    p = lane_plan("f32", 28, 2, 20, 20, reduces=True)
+    assert p["units"] == 1 << 21 and p["units"] // (4 * p["it"]) <= 2048
+    assert lane_plan("f32", 28, 2, 20, 20)["it"] == 1
+    assert lane_plan("f32", 6, 2, 1, 1) is None   # 32 chunks: too small for the family
+    lib = load("f32")
+    out = (C.c_uint * 10)()
+    assert lib.qdc_lane_plan(10, 3, 1, 1, 0, out) == -1
+    assert lib.qdc_lane_plan(10, 4, 3, 3, 0, out) == -1

@@ -47,6 +47,62 @@ __global__ __launch_bounds__(256) void k_stream(const vec4* __restrict__ a, vec4
   }
 }
 
+// Gate-shaped patterns: ROWS rows (the 2^k amplitudes a k-qubit gate couples) at a far chunk
+// stride (1 << RB).  SPLIT: one chunk per lane — lane group g = lane / (64 / ROWS) takes row g,
+// so a wave covers 64 / ROWS consecutive items of each row; else each lane loads every row of
+// its item (the single-gate direct kernels' shape: ROWS loads per lane).
+template <int ROWS, bool SPLIT, int RB>
+__global__ __launch_bounds__(256) void k_rows(vec4* __restrict__ a, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int LOGR = ROWS == 1 ? 0 : ROWS == 2 ? 1 : 2;
+  auto row_addr = [&](uint64_t item, int r) {  // item: index over n / ROWS; insert row bits
+    uint64_t x = item;
+    for (int k = 0; k < LOGR; ++k) {
+      const uint32_t b = RB + k;
+      x = ((x >> b) << (b + 1)) | (x & ((1ull << b) - 1));
+    }
+    for (int k = 0; k < LOGR; ++k) x |= (uint64_t)((r >> k) & 1) << (RB + k);
+    return x;
+  };
+  if (SPLIT) {
+    const uint32_t per = 64 / ROWS, g = lane / per, i = lane % per;
+    const uint64_t item = ((uint64_t)blockIdx.x * 4 + wave) * per + i;
+    vec4 x = ld(a + row_addr(item, (int)g));
+    x = x * 0.9999999f + x.yxwz * 1e-7f;
+    st(a + row_addr(item, (int)g), x);
+  } else {
+    const uint64_t item = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    vec4 x[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) x[r] = ld(a + row_addr(item, r));
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) st(a + row_addr(item, r), x[r] * 0.9999999f + x[(r + 1) % ROWS] * 1e-7f);
+  }
+}
+
+template <int ROWS, bool SPLIT, int RB>
+static void run_rows(vec4* a, uint64_t n) {
+  const uint32_t grid = SPLIT ? (uint32_t)(n / 256) : (uint32_t)(n / ROWS / 256);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((k_rows<ROWS, SPLIT, RB>), dim3(grid), dim3(256), 0, 0, a, n);
+  CK(hipDeviceSynchronize());
+  float best = 1e9f;
+  for (int r = 0; r < 5; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_rows<ROWS, SPLIT, RB>), dim3(grid), dim3(256), 0, 0, a, n);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (ms < best) best = ms;
+  }
+  const double tbs = 2.0 * (double)n * 16 / (best * 1e-3) / 1e12;
+  printf("rows=%d split=%d rowbit=%2d             %7.3f ms  %5.2f TB/s  %5.1f%%\n", ROWS, SPLIT ? 1 : 0,
+         RB, best, tbs, 100.0 * tbs / 8.0);
+}
+
 template <int U, bool XCD, bool NT>
 static void run(const char* name, vec4* a, vec4* b, uint64_t n) {
   const uint32_t grid = (uint32_t)(n / (256 * U));
@@ -92,6 +148,16 @@ int main() {
     run<4, false, true>("out of place", a, b, n);
     run<1, true, false>("in place", a, a, n);
     run<1, true, false>("out of place", a, b, n);
+  }
+  for (int rep = 0; rep < 2; ++rep) {
+    run_rows<2, false, 20>(a, n);
+    run_rows<2, true, 20>(a, n);
+    run_rows<2, false, 12>(a, n);
+    run_rows<2, true, 12>(a, n);
+    run_rows<4, false, 20>(a, n);
+    run_rows<4, true, 20>(a, n);
+    run_rows<4, false, 8>(a, n);
+    run_rows<4, true, 8>(a, n);
   }
   return 0;
 }
