@@ -576,19 +576,44 @@ struct RqPlan {
   std::vector<RqStep> steps;
 };
 
-// The layout's LDS descriptor (qdc_rq.hpp rq_layout): rp[j] = swz(dep(j -> slots)),
-// tv[k] = swz(1 << k-th thread bit), thread bits = tile bits not in a slot, ascending.
+// LDS index swizzle of the register-resident passes' relayouts.  A relayout writes (and reads)
+// register j of lane l at index tp(l) ^ rp[j]: a 32-lane half of a ds_write/read_b64 is
+// conflict-free when the images of lane bits 0..4 are independent mod 32 (64 banks of 4 B).
+// The lane bits are the layout's five lowest thread bits — any tile bits — so f32 index bits
+// 5..10 are XORed into bits 0..4 by the rows of RQ_SWZ, found by a search over the relayouts
+// of the C2 step's 123 specialized passes (average bank multiplicity per half 2.06 -> 1.20;
+// on a deep random circuit's 93 passes 2.28 -> 1.27; the k_fused swizzle swz, whose bits 9..10
+// map to nothing, gave 2.06).  XOR-linear, so addresses stay tp ^ rp[j]; a bijection (the high
+// bits are unchanged).  QDC_RQ_SWZ=0: swz.  f64 (16-B entries, other bank grouping): swz.
+inline bool rq_swz_on() {
+  static const bool on = [] {
+    const char* e = getenv("QDC_RQ_SWZ");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+inline uint32_t rq_swz(uint32_t i) {
+  if (LV == 0 || !rq_swz_on()) return swz(i);
+  constexpr uint32_t M[6] = {27u, 13u, 28u, 21u, 27u, 22u};
+  uint32_t x = i;
+  for (uint32_t b = 0; b < 6; ++b)
+    if ((i >> (5 + b)) & 1u) x ^= M[b];
+  return x;
+}
+
+// The layout's LDS descriptor (qdc_rq.hpp rq_layout): rp[j] = rq_swz(dep(j -> slots)),
+// tv[k] = rq_swz(1 << k-th thread bit), thread bits = tile bits not in a slot, ascending.
 inline rq_layout rq_descriptor(const RqLayout& L, uint32_t T) {
   rq_layout d{};
   for (uint32_t j = 0; j < (1u << L.ns); ++j) {
     uint32_t idx = 0;
     for (uint32_t s = 0; s < L.ns; ++s)
       if ((j >> s) & 1u) idx |= 1u << L.slot[s];
-    d.rp[j] = swz(idx);
+    d.rp[j] = rq_swz(idx);
   }
   uint32_t th[8];
   const uint32_t nt = L.threads(T, th);
-  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = swz(1u << th[k]);
+  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = rq_swz(1u << th[k]);
   return d;
 }
 // The HBM side of a load / store layout (rqio halves): chunk offsets of the thread bits and of

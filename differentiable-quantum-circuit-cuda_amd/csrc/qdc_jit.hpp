@@ -156,11 +156,11 @@ inline rq_layout rq_descriptor_without(const RqLayout& L, uint32_t T, uint32_t b
     uint32_t idx = 0;
     for (uint32_t s = 0; s < L.ns; ++s)
       if ((j >> s) & 1u) idx |= 1u << L.slot[s];
-    d.rp[j] = swz(cut(idx));
+    d.rp[j] = rq_swz(cut(idx));
   }
   uint32_t th[8];
   const uint32_t nt = L.threads(T, th);
-  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = swz(cut(1u << th[k]));
+  for (uint32_t k = 0; k < nt; ++k) d.tv[k] = rq_swz(cut(1u << th[k]));
   return d;
 }
 inline std::string spec_program_source(const std::vector<SpecStep>& steps, uint32_t T, const SpecKind& K) {
@@ -348,10 +348,10 @@ inline std::string spec_defines() {
            "-DQDC_DYN_TAIL=%d -DQDC_FMAX_OPS=%d -DQDC_FMAX_GRAD_RQ=%d -DQDC_RQ_PF_WAVES=%d "
            "-DQDC_RW_WAVES=%d -DQDC_RW_WAVES_ONE=%d -DQDC_RQ_ABL=%d -DQDC_RQ_GSPLIT=%d "
            "-DQDC_NT_LOAD=%d -DQDC_NT_STORE=%d -DQDC_RW_WAVES_HALF_ONE=%d -DQDC_PK_ASM=%d -DQDC_PK_VASM=%d "
-           "-DQDC_MATVEC_N=%d -DQDC_RW_STAGGER=%d%s",
+           "-DQDC_MATVEC_N=%d%s",
            (int)QDC_DYN_TAIL, (int)FMAX_OPS, (int)FMAX_GRAD_RQ, (int)QDC_RQ_PF_WAVES,
            (int)QDC_RW_WAVES, (int)QDC_RW_WAVES_ONE, (int)QDC_RQ_ABL, (int)QDC_RQ_GSPLIT,
-           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE, (int)QDC_PK_ASM, (int)QDC_PK_VASM, (int)QDC_MATVEC_N, (int)QDC_RW_STAGGER,
+           (int)QDC_NT_LOAD, (int)QDC_NT_STORE, (int)QDC_RW_WAVES_HALF_ONE, (int)QDC_PK_ASM, (int)QDC_PK_VASM, (int)QDC_MATVEC_N,
            sizeof(real) == 8 ? " -DQDC_F64" : "");
   return b;
 }

@@ -39,9 +39,6 @@ namespace qdc {
 #ifndef QDC_MATVEC_N
 #define QDC_MATVEC_N 1
 #endif
-#ifndef QDC_RW_STAGGER
-#define QDC_RW_STAGGER 0
-#endif
 
 constexpr int RQ_R = 16;  // amplitudes per thread per state
 constexpr uint32_t FK_RELAYOUT = 7;
@@ -787,13 +784,6 @@ __device__ __forceinline__ void rw_pass(chunk* __restrict__ f, chunk* __restrict
   if constexpr (TWO) {
     for (uint32_t i = lane; i < FMAX_GRAD_RQ * FACC; i += 64) (&accw[0][0])[i] = 0;
   }
-#if QDC_RW_STAGGER
-  // (experiment) waves in odd hardware slots (HW_ID wave_id, bits 3:0) start QDC_RW_STAGGER x
-  // 8 k cycles late, so the two waves a SIMD holds are out of phase: one loads while the other
-  // computes
-  if (W == 1 && (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 1u))
-    for (int i = 0; i < QDC_RW_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   const rqio* io = reinterpret_cast<const rqio*>(mats + l0 + sizeof(rq_layout) / sizeof(cx));
   uint64_t thr_ld = 0, thr_st = 0;  // this lane's chunk offsets in the load / store layout
 #pragma unroll
