@@ -253,8 +253,9 @@ struct Circuit {
   // (QDC_RW bit 3, with QDC_RQ_PF)
   bool rw1_prefetch() const { return (rq_wave & 8) && rq_prefetch; }
   // register-resident tile order: 0 block-contiguous, 1 grid-strided, 2 block-contiguous in
-  // XCD-aware block order (QDC_RQ_ORDER)
-  int rq_order = 0;
+  // XCD-aware block order (QDC_RQ_ORDER).  C2 n = 28, same box (profiles/r5/r5q_*): 2 is
+  // +0.4-0.6 % over 0, 1 (concurrent tiles neighbours in memory) -6.5 %
+  int rq_order = 2;
   // register-resident passes as straight-line kernels specialized per pass program
   // (qdc_spec.hpp, qdc_jit.hpp; QDC_SPEC): 0 off, 1 for states of >= spec_min_qubits local
   // qubits, 2 always; a call whose program needs more than spec_max distinct kernels runs generic
