@@ -723,7 +723,11 @@ def main():
             lib = Path(__import__("quantum_differentiable_circuit._native", fromlist=["x"]).lib_path(
                 args.precision))
             sha = hashlib.sha256(lib.read_bytes()).hexdigest()[:16]
-            if args.precision == "f32" and pmc.get("lib_sha16") == sha:
+            # the PMC passes run the default workload (C2 at n = 28): per-launch bytes of
+            # another workload or size are not this line's
+            if args.workload != "c2" or n != 28:
+                traffic_src = f"{pmc_path.name} measures the C2 n=28 step, not this workload"
+            elif args.precision == "f32" and pmc.get("lib_sha16") == sha:
                 traffic, traffic_src = pmc.get(dom_name), f"{pmc_path.name} (build {sha})"
             else:
                 traffic_src = f"{pmc_path.name} is from another build ({pmc.get('lib_sha16')} != {sha})"
