@@ -34,6 +34,7 @@ sys.path.insert(0, str(ROOT / "differentiable-quantum-circuit-cuda_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # vector peak (MI355X_MICROARCH.md; packed f32)
+XGMI_LINK_GBS = 153.0  # one xGMI link of MI355X, per direction (7 point-to-point links per GPU)
 
 
 class heartbeat:
@@ -433,14 +434,16 @@ def dense_gate_sample(args, n):
     return out
 
 
-def vqse_sample(steps=3):
-    """Config C3 (example_vqse_ising.py at its own size: n = 26, 26 layers, f64, |+>^n): wall
-    seconds per loss-and-gradient call (the number example:133 prints), and the HBM roofline and
-    f64 VALU rate of the call's dominant kernel (HIP events on the circuit's stream)."""
+def vqse_sample(precision="f64", steps=3):
+    """Config C3 (example_vqse_ising.py at its own size: n = 26, 26 layers, |+>^n) in either
+    precision — BASELINE.json names f64, the example itself runs complex64
+    (example_vqse_ising.py:58,87-89): wall seconds per loss-and-gradient call (the number
+    example:133 prints), and the HBM roofline and VALU rate of the call's dominant kernel (HIP
+    events on the circuit's stream)."""
     from qdc import AutoGradCircuit
     from quantum_differentiable_circuit import workloads as W
     n, layers = 26, 26
-    ac = AutoGradCircuit(n, precision="f64")
+    ac = AutoGradCircuit(n, precision=precision)
     ac.set_state_from_vector(np.ones(1 << n, dtype=ac.dtype) / np.sqrt(1 << n))
     for kind, pos in W.vqse_ising(n, layers):
         if kind == W.VAR_Q2_DIAG:
@@ -466,7 +469,8 @@ def vqse_sample(steps=3):
     stats = ac.circuit.profile_collect()
     ac.circuit.profile(False)
     out = {"s_per_loss_grad_call": round(dt, 4), "energy": round(e, 6), "qubits": n,
-           "layers": layers, "gates": 2 * n * layers, "dtype": "c128 (f64)", "calls": steps}
+           "layers": layers, "gates": 2 * n * layers,
+           "dtype": "c128 (f64)" if precision == "f64" else "c64 (f32)", "calls": steps}
     dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["total_ms"])
     avg = dom["total_ms"] / dom["launches"]
     gbs = dom["algo_bytes"] / dom["launches"] / (avg * 1e-3) / 1e9
@@ -480,8 +484,8 @@ def vqse_sample(steps=3):
     if dom.get("algo_flops"):
         tf = dom["algo_flops"] / dom["launches"] / (avg * 1e-3) / 1e12
         out["compute"] = {"bound": "valu", "kernel": dom_name, "achieved": round(tf, 2),
-                          "peak": VALU_PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
-                          "frac": round(tf / VALU_PEAK_TFLOPS["f64"], 4)}
+                          "peak": VALU_PEAK_TFLOPS[precision], "unit": "TFLOP/s",
+                          "frac": round(tf / VALU_PEAK_TFLOPS[precision], 4)}
     out["kernels"] = {k: {"launches": v["launches"] // steps,
                           "avg_ms": round(v["total_ms"] / v["launches"], 4)}
                       for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"])}
@@ -644,14 +648,19 @@ def main():
     # a program with more distinct specialized kernels than QDC_SPEC_MAX (C5's deep random
     # circuit) compiles them in the background while generic kernels run its passes: wait for
     # them (progress on stderr), then one more untimed step loads them
+    # The decision is collective: the extra step issues RCCL all-to-alls and all-reduces, so every
+    # rank runs it when any rank still has kernels queued, and the wait loop ends on the same
+    # iteration everywhere (max over ranks of what is left and of the time waited).
     jit_bg_s = 0.0
-    if q.jit_stats(args.precision)["queued"] > 0:
+    if max_over_ranks(float(q.jit_stats(args.precision)["queued"]), comm) > 0:
         tj = time.perf_counter()
         while True:
             left = q.jit_wait(30.0, args.precision)
             print(f"[bench] rank {rank}: {left} specialized kernels still compiling "
                   f"({time.perf_counter() - tj:.0f} s)", file=sys.stderr, flush=True)
-            if left == 0 or time.perf_counter() - tj > args.jit_wait_max_s:
+            left_all = max_over_ranks(float(left), comm)
+            waited = max_over_ranks(time.perf_counter() - tj, comm)
+            if left_all == 0 or waited > args.jit_wait_max_s:
                 break
         jit_bg_s = time.perf_counter() - tj
         with heartbeat("warm-up on the specialized passes"):
@@ -754,8 +763,33 @@ def main():
     eff = ngates * 6 * state_bytes / (elapsed / args.steps) / 1e9 / ngpu
     effective = {"per_gpu_GB/s": round(eff, 1), "x_hbm_peak": round(eff / HBM_PEAK_GBS, 3),
                  "definition": "gates x (2S fwd + 4S bwd) per step / step time, per GPU"}
-    gate_kernels = dense_kernels = vqse = abi = None
-    if rank == 0 and world == 1 and not args.no_gate_sample and args.workload == "c2":
+    # the all-to-all of sharded runs: bytes each shard sends to the others per all-to-all over
+    # the exchange's event time, per GPU, against the link it crosses (one GPU per process or
+    # per shard: xGMI; a one-GPU rehearsal: device copies through HBM)
+    exchange = None
+    a2a = stats.get("alltoall")
+    if shards > 1 and a2a and a2a["launches"] > 0 and a2a["total_ms"] > 0:
+        per_gpu = shards // ngpu  # shards a GPU holds (every shard's events span its GPU's copies)
+        avg = a2a["total_ms"] / a2a["launches"]
+        sent = a2a["algo_bytes"] / a2a["launches"] * per_gpu  # bytes per GPU per all-to-all
+        gbs = sent / (avg * 1e-3) / 1e9
+        if ngpu > 1:
+            link, peak = (f"xGMI, {ngpu - 1} of the 7 point-to-point links per GPU at "
+                          f"{XGMI_LINK_GBS:.0f} GB/s each"), (ngpu - 1) * XGMI_LINK_GBS
+        else:
+            link, peak = ("rehearsal: device copies on one GPU (each byte read and written in "
+                          "HBM)"), HBM_PEAK_GBS / 2
+        nrec = 1 if world > 1 else shards  # event records per all-to-all (one per local shard)
+        exchange = {"alltoalls_per_step": round(a2a["launches"] / args.steps / nrec, 2),
+                    "avg_ms": round(avg, 4), "bytes_per_gpu": sent,
+                    "alltoall_GB/s": round(gbs, 1), "link": link, "link_peak_GB/s": peak,
+                    "frac": round(gbs / peak, 4),
+                    "ms_per_step": round(a2a["total_ms"] / args.steps / nrec, 3)}
+
+    gate_kernels = dense_kernels = vqse = vqse32 = abi = None
+    # (the auxiliary samples and the CPU baseline belong to the one-GPU headline: a sharded run —
+    # any number of processes, GPUs or local shards — reports its own step and exchange only)
+    if rank == 0 and shards == 1 and not args.no_gate_sample and args.workload == "c2":
         # auxiliary samples: a failure there is reported in the line, never loses the headline
         def aux(fn, *a):
             try:
@@ -765,11 +799,12 @@ def main():
         with heartbeat("auxiliary samples"):
             gate_kernels = aux(gate_kernel_sweep, args, n)
             dense_kernels = aux(dense_gate_sample, args, n)
-            vqse = aux(vqse_sample)
+            vqse = aux(vqse_sample, "f64")
+            vqse32 = aux(vqse_sample, "f32")
             abi = aux(abi_unfused_sample, args, n)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and shards == 1 and not args.no_cpu_baseline:
         try:
             with heartbeat("CPU baseline (the reference's algorithm on the host cores)"):
                 cpu = cpu_baseline(args, args.cpu_qubits or n)
@@ -828,6 +863,8 @@ def main():
             "gate_kernels": gate_kernels,
             "dense_gate_kernels": dense_kernels,
             "vqse_c3": vqse,
+            "vqse_c3_f32": vqse32,
+            "exchange": exchange,
             "abi_unfused": abi,
             "cpu_baseline": cpu,
         }

@@ -646,10 +646,64 @@ QDC_API const char* qdc_precompile(size_t n, int world, const int* kinds, const 
     srcs.push_back(e->src);
   }
   if (kernels) *kernels = names.size();
+  // (QDC_PRECOMPILE_DUMP=dir: also write each kernel's source to dir/<name>.hip, in launch order
+  // of first use, with dir/order.txt — the per-pass time model joins them with a kernel trace)
+  if (const char* dd = getenv("QDC_PRECOMPILE_DUMP")) {
+    const std::string d(dd);
+    FILE* lst = fopen((d + "/order.txt").c_str(), "a");
+    for (size_t i = 0; i < names.size(); ++i) {
+      if (FILE* f = fopen((d + "/" + names[i] + ".hip").c_str(), "w")) {
+        fwrite(srcs[i].data(), 1, srcs[i].size(), f);
+        fclose(f);
+      }
+      if (lst) fprintf(lst, "%s\n", names[i].c_str());
+    }
+    if (lst) fclose(lst);
+  }
   // (QDC_PRECOMPILE_COUNT=1: count the kernels only)
   const char* co = getenv("QDC_PRECOMPILE_COUNT");
   if (names.empty() || (co && atoi(co) != 0)) return nullptr;
   return qdc::SpecJit::get().compile_only(names, srcs);
+}
+
+// host-only hooks (qdc_trace_program, qdc_check_schedule): an instruction's kind and positions
+// as qdc_circuit_push accepts them (positions < n, a two-qubit op's two positions distinct)
+static const char* check_instr(int kind, unsigned p2, unsigned p1, size_t n, size_t i) {
+  if (kind < QDC_CONST_Q2 || kind > QDC_DIFF_Q1_DENSITY)
+    return qdc::fail("unknown instruction kind %d", kind);
+  const bool q1 = qdc::is_q1_gate(kind) || qdc::is_q1_density(kind);
+  if (p2 >= n || (!q1 && (p1 >= n || p1 == p2)))
+    return qdc::fail("instruction %zu: invalid positions (%u, %u) on %zu qubits", i, p2, p1, n);
+  return nullptr;
+}
+
+QDC_API const char* qdc_trace_program(size_t n, int world, const int* kinds, const unsigned* pos2,
+                                      const unsigned* pos1, size_t count, const qdc_complex* cg,
+                                      const size_t* cl, size_t nc, const qdc_complex* vg,
+                                      const size_t* vl, size_t nv, const qdc_complex* dg,
+                                      const size_t* dl, size_t nd, qdc_trace_op* out, size_t cap,
+                                      size_t* n_out) {
+  static_assert(sizeof(qdc_trace_op) == sizeof(qdc::Circuit::TraceOp), "trace op layout");
+  if (n == 0 || n > 40 || world < 1 || !n_out || (count > 0 && (!kinds || !pos2 || !pos1)))
+    return qdc::fail("invalid trace arguments");
+  qdc::Circuit k;
+  QDC_TRY(k.init_dry((uint32_t)n, world));
+  for (size_t i = 0; i < count; ++i) {
+    const int kind = kinds[i];
+    if (const char* e = check_instr(kind, pos2[i], pos1[i], n, i)) return e;
+    const bool q1 = qdc::is_q1_gate(kind) || qdc::is_q1_density(kind);
+    k.ins.push_back({kind, pos2[i], q1 ? 0u : pos1[i]});
+  }
+  k.tracing = true;
+  qdc::Flat cf(cg, cl, nc), vf(vg, vl, nv), df(dg, dl, nd);
+  std::vector<qdc_complex> dens(std::max<size_t>(k.output_size(QDC_MODE_FORWARD), 1));
+  QDC_TRY(k.execute(QDC_MODE_FORWARD, cf, vf, dens.data()));
+  std::vector<qdc_complex> grads(std::max<size_t>(k.grad_size(), 1));
+  QDC_TRY(k.backward(df, cf, vf, grads.data()));
+  *n_out = k.trace.size();
+  for (size_t i = 0; i < k.trace.size() && i < cap; ++i)
+    std::memcpy(&out[i], &k.trace[i], sizeof(qdc_trace_op));
+  return nullptr;
 }
 
 // Host-only consistency check of the runtime's forward schedule (tests): plan the forward of a
@@ -660,9 +714,12 @@ QDC_API const char* qdc_precompile(size_t n, int world, const int* kinds, const 
 QDC_API const char* qdc_check_schedule(size_t n, int world, const int* kinds, const unsigned* pos2,
                                        const unsigned* pos1, size_t count, size_t* items_out,
                                        size_t* swaps_out) {
+  if (n == 0 || n > 40 || world < 1 || (count > 0 && (!kinds || !pos2 || !pos1)))
+    return qdc::fail("invalid schedule arguments");
   qdc::Circuit k;
   QDC_TRY(k.init_dry((uint32_t)n, world));
   for (size_t i = 0; i < count; ++i) {
+    if (const char* e = check_instr(kinds[i], pos2[i], pos1[i], n, i)) return e;
     const bool q1 = qdc::is_q1_gate(kinds[i]) || qdc::is_q1_density(kinds[i]);
     k.ins.push_back({kinds[i], pos2[i], q1 ? 0u : pos1[i]});
   }

@@ -265,8 +265,12 @@ struct Circuit {
   int spec_fwd = 1;  // forward (one-state) passes too (QDC_SPEC_FWD)
   // a program with more than spec_max distinct kernels: its missing kernels are compiled by the
   // JIT's background thread while the generic kernels run its passes, later calls launch the
-  // specialized ones as their objects appear (QDC_SPEC_ASYNC=0: such programs stay generic)
-  int spec_async = 1;
+  // specialized ones as their objects appear (QDC_SPEC_ASYNC=0: such programs stay generic).
+  // f32 only by default: f32 specialized and generic passes are bit-identical, so a result never
+  // depends on how far the background compiler has got; f64 ones differ in the last bits (the
+  // compiler contracts the scalar complex arithmetic differently), so a deep f64 program stays
+  // generic — reproducible from call to call — unless QDC_SPEC_ASYNC=1 opts in
+  int spec_async = sizeof(real) == 4 ? 1 : 0;
   // generated kernels by pass program (key: qdc_circuit build_program), with their functions
   std::map<std::vector<uint32_t>, SpecEntry> spec_cache;
   uint64_t spec_epoch = 0;
@@ -311,6 +315,17 @@ struct Circuit {
   bool dry = false;
   std::vector<unsigned char> dry_prog;
   std::vector<SpecEntry*> dry_specs;
+  // dry-run trace of the matrices a call applies to the forward state (qdc_trace_program, the
+  // host emulation tools/drift_emu.py): per fused stage or single gate its logical qubits (row
+  // index 2 bit(q2) + bit(q1); q2 == q1 for one qubit), the matrix as uploaded (working
+  // precision, diagonals expanded) and whether it is the adjoint of a recorded forward matrix
+  struct TraceOp {
+    uint32_t dir, item, q2, q1, R, diag, mirrored, single;
+    qdc_complex m[16];
+  };
+  bool tracing = false;
+  std::vector<TraceOp> trace;
+  size_t trace_from = 0;
   std::vector<uint8_t> inexact;  // per instruction: gate not unitary to working precision
   uint32_t fused_blocks = 0;  // 0: as many blocks as are resident at once (occupancy query)
   std::vector<std::pair<const void*, uint32_t>> fused_resident_cache;
@@ -1182,6 +1197,7 @@ struct Circuit {
         // (same rounding; the forward frame's two qubits may have swapped order under the
         // forward pass's permutation)
         SMat Aup = A;
+        bool from_fwd = false;
         if (backward && !it.mirror_of.empty()) {
           bool nonu = false;
           for (uint32_t pi : st) nonu = nonu || is_nonu(ins[plan[pi].instr].kind);
@@ -1213,8 +1229,19 @@ struct Circuit {
                   At.a[pp * R + qq] = std::conj(Pf.a[sq * R + sp]);
                 }
               Aup = At;
+              from_fwd = true;
             }
           }
+        }
+        if (tracing) {  // (physical positions; trace_logical maps them to logical qubits)
+          TraceOp t{backward ? 1u : 0u, (uint32_t)ii, hi, lo, (uint32_t)R, all_diag ? 1u : 0u,
+                    from_fwd ? 1u : 0u, 0u, {}};
+          for (int i = 0; i < R * R; ++i) {
+            const bool keep = !all_diag || i % (R + 1) == 0;
+            t.m[i].re = keep ? (qdc_real)(real)Aup.a[i].real() : 0;
+            t.m[i].im = keep ? (qdc_real)(real)Aup.a[i].imag() : 0;
+          }
+          trace.push_back(t);
         }
         pf.emplace_back();
         pslot.push_back(-1);
@@ -1826,6 +1853,77 @@ struct Circuit {
     return apply_dense<4>(ctx, s, a, p2, p1, nl, uncompute ? "uncompute_q2" : "apply_q2");
   }
 
+  // The trace entries of this call's fused stages (build_program, physical positions) mapped to
+  // logical qubits by replaying the call's layout changes (remaps, undone remaps, permuting
+  // passes' swaps) from `layout` (the call's start), with the single-gate items' matrices (as
+  // apply_gate / reverse_dense apply them) inserted in item order.  Dry runs only.
+  const char* trace_logical(const std::vector<Item>& items, const std::vector<qdc_plan_op>& pl,
+                            bool backward, const Flat& cg, const Flat& vg,
+                            const std::vector<size_t>& gidx) {
+    std::vector<TraceOp> fused(trace.begin() + (std::ptrdiff_t)trace_from, trace.end());
+    trace.resize(trace_from);
+    QubitMap m = layout;
+    size_t t = 0;
+    for (size_t ii = 0; ii < items.size(); ++ii) {
+      const Item& it = items[ii];
+      for (; t < fused.size() && fused[t].item == ii; ++t) {
+        TraceOp s = fused[t];
+        s.q2 = m.logi[s.q2];
+        s.q1 = m.logi[s.q1];
+        trace.push_back(s);
+      }
+      if (it.type == 1) {
+        const qdc_plan_op& op = pl[it.ops[0]];
+        if (it.inv)
+          m.unapply(op.victims);
+        else
+          m.apply(op.victims);
+      } else if (it.type == 0) {
+        const qdc_plan_op& op = pl[it.ops[0]];
+        const Instr& in = ins[op.instr];
+        if (is_const(in.kind) || is_var(in.kind)) {
+          const qdc_complex* g4 = is_const(in.kind) ? cg.at(gidx[op.instr]) : vg.at(gidx[op.instr]);
+          TraceOp s{backward ? 1u : 0u, (uint32_t)ii, m.logi[op.pos2], m.logi[op.pos1], 4u,
+                    is_diag(in.kind) ? 1u : 0u, 0u, 1u, {}};
+          auto put = [&](const cx* a, int R) {
+            s.R = (uint32_t)R;
+            for (int i = 0; i < R * R; ++i) s.m[i] = qdc_complex{(qdc_real)a[i].x, (qdc_real)a[i].y};
+          };
+          if (is_diag(in.kind)) {
+            const diag4 d0 = to_diag(g4);
+            const diag4 d = backward ? conj_diag(d0) : d0;
+            for (int i = 0; i < 4; ++i) s.m[i * 5] = qdc_complex{(qdc_real)d.a[i].x, (qdc_real)d.a[i].y};
+          } else if (is_q1_gate(in.kind)) {
+            const mat<2> u = to_mat<2>(g4);
+            mat<2> a = u;
+            if (backward) {
+              if (is_nonu(in.kind))
+                QDC_TRY(inverse<2>(u, a));
+              else
+                a = conj_transpose<2>(u);
+            }
+            s.q1 = s.q2;
+            put(a.a, 2);
+          } else {
+            const mat<4> u = to_mat<4>(g4);
+            mat<4> a = u;
+            if (backward) {
+              if (is_nonu(in.kind))
+                QDC_TRY(inverse<4>(u, a));
+              else
+                a = conj_transpose<4>(u);
+            }
+            put(a.a, 4);
+          }
+          trace.push_back(s);
+        }
+      }
+      for (const auto& sw : it.swaps) m.swap_phys(sw.first, sw.second);
+    }
+    trace_from = trace.size();
+    return nullptr;
+  }
+
   const char* dyn_reset_all() {
     for (auto& d : devs) {
       QDC_TRY(d->ctx.use());
@@ -1887,6 +1985,7 @@ struct Circuit {
       fprintf(stderr, "forward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     if (dry) {  // the layout the passes leave (permuting passes' swaps, remaps), no launch
+      if (tracing) QDC_TRY(trace_logical(items, pl, false, cg, vg, gidx));
       for (const Item& item : items) {
         for (const auto& sw : item.swaps) layout.swap_phys(sw.first, sw.second);
         if (item.type == 1) layout.apply(pl[item.ops[0]].victims);
@@ -2097,7 +2196,7 @@ struct Circuit {
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
                           (uint32_t)nvar, {}, &dg));
     ht[3] = hclock::now();
-    if (dry) return nullptr;
+    if (dry) return tracing ? trace_logical(items, pl, true, cg, vg, gidx) : nullptr;
     if (rq_stats)
       fprintf(stderr, "backward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());

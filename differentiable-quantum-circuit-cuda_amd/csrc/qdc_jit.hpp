@@ -561,10 +561,13 @@ class SpecJit {
   std::set<std::string> pending;
   bool worker_on = false;
   // Background compiles, one batch of the compile parallelism at a time under the lock (ensure()
-  // and the runtime wait at most one batch: seconds); exits when the queue is empty or
-  // specialization was switched off.
+  // and the runtime wait at most one batch: seconds); kernels another process of the job is
+  // compiling are not waited for under the lock (their flock waits can last minutes) but queued
+  // again behind the rest, and a batch of nothing but those sleeps without the lock; exits when
+  // the queue is empty or specialization was switched off.
   void background() {
     for (;;) {
+      bool idle = false;
       {
         std::lock_guard<std::mutex> lk(mu);
         if (queue.empty() || state <= 0) {
@@ -586,11 +589,20 @@ class SpecJit {
           todo.push_back(k);
           queue.pop_front();
         }
-        (void)obtain(names, srcs, todo);  // (a failure disables specialization: loop ends)
-        for (const std::string& nm : names) pending.erase(nm);
+        std::vector<size_t> deferred;
+        (void)obtain(names, srcs, todo, &deferred);  // (a failure disables specialization: loop ends)
+        std::vector<bool> again(names.size(), false);
+        for (size_t k : deferred) {
+          again[k] = true;
+          queue.push_back({names[k], srcs[k]});
+        }
+        for (size_t k = 0; k < names.size(); ++k)
+          if (!again[k]) pending.erase(names[k]);
         stats.queued = pending.size();
+        idle = !deferred.empty() && deferred.size() == names.size();
       }
       cv.notify_all();
+      if (idle) usleep(50000);
     }
   }
   std::map<std::pair<int, std::string>, hipFunction_t> loaded;
@@ -789,8 +801,10 @@ class SpecJit {
   // when every remaining kernel is held by another process, wait for one, then load it — or
   // compile it here if that process failed.  So the ranks of a job share the compiles instead of
   // the first one taking them all.
+  // deferred (background compiler): kernels left only because other processes hold their
+  // locks are returned there instead of waited for
   bool obtain(const std::vector<std::string>& names, const std::vector<std::string>& srcs,
-              const std::vector<size_t>& todo) {
+              const std::vector<size_t>& todo, std::vector<size_t>* deferred = nullptr) {
     auto lock_fd = [&](size_t i) {
       return open(lock_path(names[i]).c_str(), O_RDWR | O_CREAT | O_CLOEXEC | O_NOFOLLOW, 0600);
     };
@@ -839,6 +853,10 @@ class SpecJit {
         continue;
       }
       if (left.empty()) break;
+      if (deferred) {
+        *deferred = left;
+        return true;
+      }
       // every remaining kernel is being compiled elsewhere: wait for the first of them
       const size_t i = left.front();
       const int fd = lock_fd(i);

@@ -515,6 +515,38 @@ def precompile(qubits_number, instructions, const_gates, var_gates, grads_wrt_de
     return int(count.value)
 
 
+def trace_program(qubits_number, instructions, const_gates, var_gates, grads_wrt_density,
+                  world=1, precision=None):
+    """Every matrix a forward call then a backward call apply to the forward state, in order, as
+    the runtime's own dry run builds them (qdc_trace_program; host only, no GPU): a numpy
+    record array with fields dir (0 forward, 1 uncompute), item, q2, q1 (logical qubits; row
+    index 2 bit(q2) + bit(q1)), R, diag, mirrored, single and m (R x R in m[:R*R], working
+    precision).  For the host drift emulation (tools/drift_emu.py)."""
+    prec = precision or default_precision()
+    lib = load(prec)
+    dt = np.dtype(PRECISIONS[prec])
+    rec = np.dtype([("dir", "<u4"), ("item", "<u4"), ("q2", "<u4"), ("q1", "<u4"), ("R", "<u4"),
+                    ("diag", "<u4"), ("mirrored", "<u4"), ("single", "<u4"), ("m", dt, 16)])
+    m = len(instructions)
+    kinds = (C.c_int * m)(*[int(i[0]) for i in instructions])
+    a = (C.c_uint * m)(*[int(i[1]) for i in instructions])
+    b = (C.c_uint * m)(*[int(i[2]) if len(i) > 2 else 0 for i in instructions])
+    cf, cl = _flat_gates(const_gates, dt, "const_gates")
+    vf, vl = _flat_gates(var_gates, dt, "var_gates")
+    dens = [_array2(g, dt, "grads_wrt_density") for g in grads_wrt_density]
+    df, dl = _flatten(dens, dt, "grads_wrt_density", "Gradient is not contiguous.")
+    cap = 4 * m + 64
+    while True:
+        out = np.zeros(cap, dtype=rec)
+        cnt = C.c_size_t(0)
+        check(lib.qdc_trace_program(int(qubits_number), int(world), kinds, a, b, m, ptr(cf),
+                                    ptr(cl), len(const_gates), ptr(vf), ptr(vl), len(var_gates),
+                                    ptr(df), ptr(dl), len(dens), ptr(out), cap, C.byref(cnt)))
+        if cnt.value <= cap:
+            return out[:cnt.value]
+        cap = cnt.value
+
+
 def jit_dir(precision=None):
     """The specialized-kernel cache directory in use; RuntimeError when specialization is off."""
     lib = load(precision or default_precision())

@@ -36,7 +36,7 @@ RUNTIME = (
     "qdc_circuit_layout", "qdc_circuit_get_shard", "qdc_circuit_get_range", "qdc_plan", "qdc_fusion_schedule",
     "qdc_rq_plan", "qdc_spec_selftest", "qdc_gate_plan", "qdc_lane_plan", "qdc_qkgate", "qdc_abi_sync", "qdc_abi_profile", "qdc_abi_profile_collect",
     "qdc_jit_stats", "qdc_jit_dir", "qdc_spec_fingerprint", "qdc_spec_selftest_batch",
-    "qdc_jit_wait", "qdc_precompile", "qdc_check_schedule",
+    "qdc_jit_wait", "qdc_precompile", "qdc_check_schedule", "qdc_trace_program",
 )
 
 
@@ -140,6 +140,9 @@ def _proto(lib):
         "qdc_precompile": (_E, [_S, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint),
                                 C.POINTER(C.c_uint), _S, _P, _P, _S, _P, _P, _S, _P, _P, _S,
                                 C.POINTER(C.c_size_t)]),
+        "qdc_trace_program": (_E, [_S, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint),
+                                   C.POINTER(C.c_uint), _S, _P, _P, _S, _P, _P, _S, _P, _P, _S,
+                                   _P, _S, C.POINTER(C.c_size_t)]),
         "qdc_spec_fingerprint": (_E, [C.c_char_p, C.c_char_p, C.c_char_p,
                                       C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
         "qdc_rq_plan": (_S, [C.c_uint, C.c_uint, C.POINTER(C.c_uint), C.POINTER(C.c_uint),

@@ -113,7 +113,11 @@ def exchange_id(rank: int, path: Path, make_id, timeout: float = 300.0, skew: fl
             data = path.read_bytes()
             if len(data) == _ID_LEN + struct.calcsize(_FMT):
                 t_root, pid, ns_root, h = struct.unpack(_FMT, data[_ID_LEN:])
-                same = h.rstrip(b"\0") == host and ns_root == ns and ns != 0
+                # rank 0's pid is checked on the same host in the same PID namespace; when
+                # either namespace is unknown (0), the host name alone decides (the old rule),
+                # so only namespaces known to differ skip the liveness check
+                known = ns != 0 and ns_root != 0
+                same = h.rstrip(b"\0") == host and (ns_root == ns or not known)
                 live = not same or _alive(pid)
                 if abs(t_root - start) <= skew and live:
                     return data[:_ID_LEN]

@@ -303,6 +303,28 @@ const char* qdc_check_schedule(size_t qubits_number, int world, const int* kinds
                                const unsigned* pos2, const unsigned* pos1, size_t count,
                                size_t* items, size_t* swaps);
 
+/* One matrix a call applies to the forward state (qdc_trace_program): dir 0 forward, 1 the
+ * backward's uncompute; its logical qubits q2, q1 (row index 2 bit(q2) + bit(q1); q2 == q1 and
+ * R == 2 for one qubit); m: the R x R row-major matrix as the kernels apply it (working precision,
+ * diagonals expanded); mirrored: the exact adjoint of the forward's recorded stage matrix;
+ * single: a single-gate item, else a fused stage; item: its pass in the call's schedule. */
+typedef struct qdc_trace_op {
+  unsigned dir, item, q2, q1, R, diag, mirrored, single;
+  qdc_complex m[16];
+} qdc_trace_op;
+
+/* Test hook (host only, the drift emulator tools/drift_emu.py): a dry run of forward(cg, vg)
+ * then backward(dg, cg, vg) as qdc_precompile, returning every matrix the two calls apply to the
+ * forward state, in order, into out[0..cap).  *count: the number of matrices (when > cap, call
+ * again with a larger buffer).  Returns NULL, or an error message. */
+const char* qdc_trace_program(size_t qubits_number, int world, const int* kinds,
+                              const unsigned* pos2, const unsigned* pos1, size_t count,
+                              const qdc_complex* const_gates, const size_t* const_lens,
+                              size_t n_const, const qdc_complex* var_gates,
+                              const size_t* var_lens, size_t n_var, const qdc_complex* dens_grads,
+                              const size_t* dens_lens, size_t n_dens, qdc_trace_op* out, size_t cap,
+                              size_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

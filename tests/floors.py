@@ -31,6 +31,15 @@ def flat(xs):
     return np.concatenate([np.asarray(x).reshape(-1) for x in xs]) if len(xs) else np.zeros(0)
 
 
+def l2rel(a, b):
+    """2-norm relative error ||a - b|| / ||b||: an aggregate over every element, so one circuit's
+    value is a stable statistic of its rounding (the max-norm of normrel is the extreme of 2^n
+    random-walk endpoints and varies ~0.3-2x between realizations, tools/drift_trace.py)."""
+    a, b = flat(a).astype(np.complex128), flat(b).astype(np.complex128)
+    den = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / den) if den > 0 else float(np.linalg.norm(a - b))
+
+
 def normrel(a, b):
     a, b = flat(a).astype(np.complex128), flat(b).astype(np.complex128)
     den = np.abs(b).max() if b.size else 0.0
@@ -98,6 +107,7 @@ class Floor:
                              run=run)
         self.exact = exact
         self.floor = {k: normrel(ref[k], exact[k]) for k in exact if k != "cots"}
+        self.floor_l2 = {k: l2rel(ref[k], exact[k]) for k in exact if k != "cots"}
 
     def check(self, key, got, what="", ratio=RATIO):
         err = normrel(got, self.exact[key])
@@ -109,6 +119,19 @@ class Floor:
               f"ratio {err / fl if fl > 0 else float('inf'):.2f}  bound {bound:.3e}  "
               f"passes-by {binding}")
         assert err <= bound, f"{what}{key}: error {err:.3e} > {ratio} x floor {fl:.3e} + atol"
+        return err
+
+
+    def check_l2(self, key, got, what="", ratio=RATIO):
+        """As check, in the 2-norm: the stable aggregate of the same rounding (state outputs)."""
+        err = l2rel(got, self.exact[key])
+        fl = self.floor_l2[key]
+        bound = ratio * fl + ATOL[self.prec]
+        binding = "floor" if err <= ratio * fl else "ATOL"
+        print(f"[floor-l2] {what}{key}: err {err:.3e}  floor {fl:.3e}  "
+              f"ratio {err / fl if fl > 0 else float('inf'):.2f}  bound {bound:.3e}  "
+              f"passes-by {binding}")
+        assert err <= bound, f"{what}{key}: 2-norm error {err:.3e} > {ratio} x floor {fl:.3e} + atol"
         return err
 
 

@@ -122,6 +122,7 @@ C_TO_RUST = {
     "qdc_circuit**": "*mut *mut QdcCircuit", "qdc_comm*": "*mut QdcComm",
     "qdc_comm**": "*mut *mut QdcComm", "qdc_kernel_stat*": "*mut QdcKernelStat",
     "qdc_plan_op*": "*mut QdcPlanOp", "const qdc_plan_op*": "*const QdcPlanOp",
+    "qdc_trace_op*": "*mut QdcTraceOp",
 }
 
 

@@ -4,7 +4,10 @@ each q1 position and every ordered q2 pair at n = 7 (one 64-chunk unit in f32), 
 (the block-wide variant's 1024-chunk units from n = 11 in f32) — targets inside the chunk (f32
 qubit 0), at near lane bits and at far lane bits — for gate
 application, densities and gradients (primitives.cu:513-646, 689-837, 202-354 via the
-primitives ABI).  Tolerances as test_gpu_primitives: 1e-5 (f32), 1e-12 (f64) relative."""
+primitives ABI).  Tolerances as test_gpu_primitives: 1e-5 (f32), 1e-12 (f64) relative.
+The default knob (QDC_LANE=2) runs application and injections on LANE and the other op classes
+on the tile / direct families; test_lane_every_op_class repeats the placements with every class
+on LANE (QDC_LANE=7), the runtime's reverse kernels included."""
 import numpy as np
 import pytest
 
@@ -29,6 +32,13 @@ def relerr(got, want):
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 @pytest.mark.parametrize("n", [7, 9, 12, 14])
 def test_lane_kernels_every_placement(prec, n):
+    bad = _placement_failures(prec, n)
+    assert not bad, f"{len(bad)} failing cells: " + "; ".join(bad[:40])
+
+
+def _placement_failures(prec, n):
+    """Every q1 position and ordered q2 pair through the primitives ABI: application, densities
+    and gradients against the oracle; the failing cells."""
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(100 + n)
     st = rnd(rng, 1 << n, prec)
@@ -67,4 +77,74 @@ def test_lane_kernels_every_placement(prec, n):
                 e = relerr(got, want)
                 if not e <= TOL[prec]:
                     bad.append(f"q2 {k} ({pos2},{pos1}) err={e:.2e}")
+    return bad
+
+
+def _reverse_failures(prec, n):
+    """The runtime's single-gate reverse kernels (uncompute + gradient + pull-back, fusion off)
+    at every q1 position and ordered q2 pair (dense and diagonal): gradients and the uncomputed
+    state against the oracle's circuit (src/circuit.rs:266-429)."""
+    import quantum_differentiable_circuit as q
+    rng = np.random.default_rng(7 + n)
+    ins, var = [], []
+    for pos in range(n):
+        ins.append((O.VAR_Q1, (pos,)))
+        var.append(O.haar_unitary(rng, 2))
+    for pos2 in range(n):
+        for pos1 in range(n):
+            if pos2 != pos1:
+                ins += [(O.VAR_Q2, (pos2, pos1)), (O.VAR_Q2_DIAG, (pos2, pos1))]
+                var += [O.haar_unitary(rng, 4), np.exp(1j * rng.standard_normal(4))]
+    ins += [(O.DIFF_Q1_DENSITY, (p,)) for p in range(n)]
+    vg = [np.ascontiguousarray(g, dtype=DT[prec]) for g in var]
+    c = q.circuit_class(prec)(n)
+    o = O.OracleCircuit(n)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+        o.add(kind, *pos)
+    d = c.forward([], vg)
+    od = o.forward([], [g.astype(np.complex128) for g in vg])
+    cots = [np.ascontiguousarray(np.diag([1.0, -1.0]), dtype=DT[prec]) for _ in d]
+    g = np.concatenate([x.reshape(-1) for x in c.backward(cots, [], vg)])
+    og = np.concatenate([np.asarray(x).reshape(-1) for x in
+                         o.backward([x.astype(np.complex128) for x in cots], [],
+                                    [g.astype(np.complex128) for g in vg])])
+    bad = []
+    # (a circuit of n + 2 n (n - 1) gates: the f32 rounding grows with its depth)
+    tol = TOL[prec] * (20 if prec == "f32" else 1)
+    for k, got, want in (("densities", np.concatenate([x.reshape(-1) for x in d]),
+                          np.concatenate([np.asarray(x).reshape(-1) for x in od])),
+                         ("grads", g, og), ("uncomputed", c.get_state(0), o.state)):
+        e = relerr(got, want)
+        if not e <= tol:
+            bad.append(f"reverse {k} err={e:.2e}")
+    return bad
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_lane_every_op_class(prec):
+    """QDC_LANE=7: every single-gate op class on the LANE family — application and injections
+    (the default), the reverse with its gradient (bit 0) and densities and gradients (bit 2) —
+    against the oracle at every placement (n = 9: in-chunk, near and far lane bits; n = 12: the
+    block-wide variant), through the primitives ABI and the runtime with fusion off.  In a child
+    process: the knob is read when a device context is created (qdc_device.hpp)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    here = Path(__file__).resolve().parent
+    code = (f"import sys, json; sys.path[:0] = [{str(here)!r}, {str(here.parent)!r}, "
+            f"{str(here.parent / 'differentiable-quantum-circuit-cuda_amd')!r}]\n"
+            "import test_gpu_lane as t\n"
+            f"bad = []\n"
+            f"for n in (9, 12):\n"
+            f"    bad += t._placement_failures({prec!r}, n) + t._reverse_failures({prec!r}, n)\n"
+            "print(json.dumps(bad))\n")
+    env = dict(os.environ, QDC_LANE="7", QDC_FUSE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    bad = json.loads(r.stdout.strip().splitlines()[-1])
+    print(f"[lane] QDC_LANE=7 {prec}: {len(bad)} failing cells")
     assert not bad, f"{len(bad)} failing cells: " + "; ".join(bad[:40])

@@ -40,10 +40,19 @@ def test_mirror_c5_depth_10k_gates(strict_mirror, prec):
     c = build(prec, n, ins)
     what = f"mirror C5 n={n} 10k {prec} "
     fl.check("forward", c.forward([], fl.var), what)
-    fl.check("state", c.get_state(0), what)
+    _check_states(fl, c, what, "state")
     fl.check("grads", c.backward(fl.cots, [], fl.var), what)
-    fl.check("uncomputed", c.get_state(0), what)
-    fl.check("bwd", c.get_state(2), what)
+    _check_states(fl, c, what, "uncomputed", "bwd")
+
+
+def _check_states(fl, c, what, *keys):
+    """Max-norm floor lines and their 2-norm counterparts (the stable aggregate: the max-norm
+    ratio of one circuit spreads ~0.3-2x with the rounding's realization — tools/drift_trace.py
+    emulates the runtime's own program on the host, DESIGN.md "Uncompute drift on shards")."""
+    for key in keys:
+        st = c.get_state(2 if key == "bwd" else 0)
+        fl.check(key, st, what)
+        fl.check_l2(key, st, what)
 
 
 @pytest.fixture(scope="module")
@@ -72,12 +81,11 @@ def test_c5_depth_10k_gates_sharded(strict_mirror, c5_floors, prec, kw):
     assert world == nloc == len(kw.get("devices", [None])) * kw.get("local_shards", 1)
     what = f"mirror C5 n={n} 10k {prec} {kw} "
     fl.check("forward", c.forward([], fl.var), what)
-    fl.check("state", c.get_state(0), what)
+    _check_states(fl, c, what, "state")
     assert c.layout()[0] != list(range(n)), "the forward must have remapped"
     fl.check("grads", c.backward(fl.cots, [], fl.var), what)
     assert c.layout()[0] == list(range(n)), "every remap undone"
-    fl.check("uncomputed", c.get_state(0), what)
-    fl.check("bwd", c.get_state(2), what)
+    _check_states(fl, c, what, "uncomputed", "bwd")
 
 
 def test_push_between_forward_and_backward():

@@ -117,6 +117,11 @@ def test_rccl_id_bootstrap_ignores_a_dead_launch(tmp_path):
     # /tmp): the pid means nothing here, the start time alone decides
     path.write_bytes(b"p" * 128 + struct.pack(D._FMT, now, dead.pid, ns + 1, host))
     assert D.exchange_id(1, path, None, timeout=1, start=now) == b"p" * 128
+    # an unknown namespace (0: /proc/self/ns/pid not readable) on the same host: the old rule,
+    # rank 0's pid must be alive
+    path.write_bytes(b"z" * 128 + struct.pack(D._FMT, now, dead.pid, 0, host))
+    with pytest.raises(TimeoutError):
+        D.exchange_id(1, path, None, timeout=0.3, start=now)
     assert D.exchange_id(0, path, lambda: b"n" * 128, start=now) == b"n" * 128
     assert D.exchange_id(1, path, None, timeout=1, start=now) == b"n" * 128
     # an id of a launch that started long before this rank: rejected
