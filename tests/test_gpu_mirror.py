@@ -45,14 +45,24 @@ def test_mirror_c5_depth_10k_gates(strict_mirror, prec):
     _check_states(fl, c, what, "uncomputed", "bwd")
 
 
+# The uncomputed state's max-norm error is the extreme of 2^n rounding random walks around
+# |0..0>: one circuit's value depends on the realization, not only on the algorithm.  The
+# reference's own gate-by-gate algorithm on C5 n = 14 (seed 33) gives max-norm 1.41e-7 in the C
+# restatement (the floor) and 7.16e-7 with numpy's complex64 arithmetic — 5x apart — but 2-norm
+# 6.17e-6 and 6.93e-6; the runtime's own program emulated on the host (tools/drift_trace.py,
+# profiles/r6/r6_drift_trace_c5_n14.txt) spreads 0.3-2.2x in max-norm and 0.85-0.92x in 2-norm
+# over 8 circuits and 1 / 2 / 8 shards.  So the 2-norm carries the claim (<= 2x the floor), and
+# the max-norm of the uncomputed state is held to 2 RATIO (a localised error would exceed both).
+UNCOMPUTED_MAX_RATIO = 2 * F.RATIO
+L2_RATIO = 2.0
+
+
 def _check_states(fl, c, what, *keys):
-    """Max-norm floor lines and their 2-norm counterparts (the stable aggregate: the max-norm
-    ratio of one circuit spreads ~0.3-2x with the rounding's realization — tools/drift_trace.py
-    emulates the runtime's own program on the host, DESIGN.md "Uncompute drift on shards")."""
+    """Max-norm floor lines and their 2-norm counterparts (the stable aggregate)."""
     for key in keys:
         st = c.get_state(2 if key == "bwd" else 0)
-        fl.check(key, st, what)
-        fl.check_l2(key, st, what)
+        fl.check(key, st, what, ratio=UNCOMPUTED_MAX_RATIO if key == "uncomputed" else F.RATIO)
+        fl.check_l2(key, st, what, ratio=L2_RATIO)
 
 
 @pytest.fixture(scope="module")

@@ -63,9 +63,24 @@ def main():
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
+    # kernel names under rocprofv3 can differ from the dry run's (the fingerprint sees the
+    # profiler's environment): map them by first use, the dry run's order.txt order
+    order = (dump / "order.txt").read_text().split()
+    first = []
+    for _, _, name in rows:
+        base = name.split("(")[0].strip()
+        if base.startswith("qdc_spec") and base not in first:
+            first.append(base)
+    if set(first) <= set(feat):
+        alias = {k: k for k in first}
+    else:
+        assert len(first) == len(order), (len(first), len(order))
+        for a, b in zip(first, order):
+            assert a.split("_")[1] == b.split("_")[1], (a, b)  # spec / specf kinds in step
+        alias = dict(zip(first, order))
     per = defaultdict(list)
     for s, e, name in rows:
-        base = name.split("(")[0].strip()
+        base = alias.get(name.split("(")[0].strip())
         if base in feat:
             per[base].append((e - s) * 1e-6)
     # the timed steps' dispatches: the median duration of each reverse kernel (launched once per
