@@ -468,6 +468,7 @@ QDC_API size_t qdc_fusion_schedule(size_t local_qubits, int backward, size_t fir
   if (const char* e = getenv("QDC_DEFER_Q1")) P.defer_q1 = atoi(e) != 0;
   if (const char* e = getenv("QDC_RQ_PERM_LOW")) P.perm_low = (uint32_t)atoi(e);
   if (const char* e = getenv("QDC_RQ_GSTAGE")) P.gamma_stage_cap = atoi(e) != 0;
+  if (const char* e = getenv("QDC_DENS_SPLIT")) P.split_dens = atoi(e) != 0;
   std::vector<qdc_plan_op> pl(plan, plan + n_plan);
   const std::vector<qdc::FusionItem> items = P.fuse_items(pl, backward != 0, first_inject);
   size_t ns = 0, no = 0;

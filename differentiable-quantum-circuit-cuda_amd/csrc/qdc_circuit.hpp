@@ -288,6 +288,10 @@ struct Circuit {
   // runs of cotangent injections whose cotangents are all diagonal become one elementwise pass
   // (k_diag_inject; QDC_DIAG_INJECT)
   int diag_inject = 1;
+  // read-only passes of one-qubit densities on k_dens1 (register partial sums across a block's
+  // tiles, one reduction per block; QDC_DENS1=0: k_fused's per-tile reductions)
+  int dens1_kernel = 1;
+  int dens_split = 1;  // forward passes hold gates or densities, not both (qdc_fusion.hpp split_dens)
   // Mirrored schedules (QDC_MIRROR): the forward is scheduled on the two-state tile under both
   // directions' rules (qdc_fusion.hpp FusionPlanner::mirror) and the backward runs its passes in
   // reverse, uncomputing each stage with exactly the adjoint of the matrix the forward applied —
@@ -424,6 +428,8 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
+    if (const char* e = getenv("QDC_DENS1")) dens1_kernel = atoi(e);
+    if (const char* e = getenv("QDC_DENS_SPLIT")) dens_split = atoi(e);
     if (const char* e = getenv("QDC_MIRROR")) mirror = atoi(e);
     if (const char* e = getenv("QDC_SPEC_HALF")) spec_half = atoi(e);
     if (const char* e = getenv("QDC_DEFER_Q1")) defer_q1 = atoi(e);
@@ -762,6 +768,7 @@ struct Circuit {
     bool rq = false;   // register-resident pass (qdc_rq.hpp): k_rq, ops include relayouts
     bool s5 = false;   // rq with five register slots (k_rw<true, 2, false, 1, true>)
     bool inv = false;  // a remap (type 1) run backwards: a mirrored backward undoing the forward's remap
+    bool dens1 = false;  // a read-only pass of one-qubit densities only: k_dens1
     uint32_t l0 = 0;   // rq: matrix-area offset (cx) of the L0 layout descriptor
     uint32_t tbits = 0;  // amplitude bits of the tile
     // specialized kernel of a five-slot reverse pass or a one-state forward pass (qdc_jit.hpp): name, source, function
@@ -883,6 +890,7 @@ struct Circuit {
     P.mirror = mirror_on() && sched_mirror;
     P.defer_q1 = defer_q1 != 0;
     P.gamma_stage_cap = rq_gstage != 0;
+    P.split_dens = dens_split != 0;
     return P;
   }
   bool is_meas(const qdc_plan_op& op) const { return planner().is_meas(op); }
@@ -1291,6 +1299,9 @@ struct Circuit {
       if (!rq) {
         for (const fop& F : pf) fops[fo++] = F;
         it.nstage = (uint32_t)pf.size();
+        bool d1 = dens1_kernel && !two && !it.writes_f && !pf.empty() && pf.size() <= (size_t)DENS1_MAX;
+        for (const fop& F : pf) d1 = d1 && (F.kind & 7u) == FK_DENS1;
+        it.dens1 = d1;
         continue;
       }
       auto put_layout = [&](const RqLayout& L) {
@@ -1556,6 +1567,36 @@ struct Circuit {
     return ctx.launch_block(name, bytes, kern, grid, (uint32_t)NT, f, b, fops, mats, g, partials,
                             stride);
   }
+  // a density-only pass (k_dens1): the tile of the one-state LDS kernel of its size
+  const char* launch_dens1(Ctx& ctx, const char* name, double bytes, const fgeo& fg, chunk* f,
+                           const fop* fops, cx* partials, uint64_t stride) {
+    if ((1ull << (fg.lc + fg.h)) == TILE_CHUNKS_2)
+      return launch_dens1_tb<(int)TILE_CHUNKS_2>(ctx, name, bytes, fg, f, fops, partials, stride);
+    return launch_dens1_tb<(int)TILE_CHUNKS_1>(ctx, name, bytes, fg, f, fops, partials, stride);
+  }
+  template <int TB>
+  const char* launch_dens1_tb(Ctx& ctx, const char* name, double bytes, const fgeo& fg, chunk* f,
+                              const fop* fops, cx* partials, uint64_t stride) {
+    if ((1ull << (fg.lc + fg.h)) != (uint64_t)TB)
+      return fail("internal: a %llu-chunk density tile on the %d-chunk kernel",
+                  (unsigned long long)(1ull << (fg.lc + fg.h)), TB);
+    if (fg.nops == 0 || fg.nops > (uint32_t)DENS1_MAX || fg.ngrad != fg.nops)
+      return fail("internal: a density pass of %u ops, %u reductions", fg.nops, fg.ngrad);
+    constexpr int NT = 256;
+    auto kern = k_dens1<TB, NT>;
+    uint32_t grid = 0;
+    QDC_TRY(fused_grid(fg, (const void*)kern, NT, grid));
+    fgeo g = fg;
+    uint64_t tpb = 1;
+    while (tpb * grid < g.ntiles) tpb <<= 1;
+    g.tpb = (uint32_t)tpb;
+    grid = (uint32_t)((g.ntiles + tpb - 1) / tpb);
+    if (grid > NBMAX) return fail("density reduction grid %u exceeds %u", grid, NBMAX);
+    last_fused_grid = grid;
+    last_fused_ndyn = 0;
+    return ctx.launch_block(name, bytes, kern, grid, (uint32_t)NT, (const chunk*)f, fops, g,
+                            partials, stride);
+  }
   // register-resident pass (qdc_rq.hpp): threads per tile = tile amplitudes / RQ_R
   const char* launch_rq(Ctx& ctx, const char* name, double bytes, const fgeo& fg, bool two,
                         uint32_t tbits, uint32_t l0, chunk* f, chunk* b, const fop* fops,
@@ -1808,6 +1849,8 @@ struct Circuit {
           QDC_TRY((launch_fused<true, true, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
         else
           QDC_TRY((launch_fused<true, false, false>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
+      } else if (it.dens1) {
+        QDC_TRY(launch_dens1(ctx, name, bytes, fg, f, fops, parts, stride));
       } else if (!it.has_red) {
         QDC_TRY((launch_fused<false, false, true>(ctx, name, bytes, fg, f, b, fops, mats, parts, stride)));
       } else if (it.writes_f) {

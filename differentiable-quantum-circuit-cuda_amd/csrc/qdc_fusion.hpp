@@ -98,6 +98,11 @@ struct FusionPlanner {
   // trailing one-qubit stages move to the pass of their qubit's next two-qubit gate
   // (defer_trailing_q1; QDC_DEFER_Q1)
   bool defer_q1 = true;
+  // a forward pass holds gates or densities, not both (round 6; QDC_DENS_SPLIT): a pass with
+  // densities cannot be register-resident, so a mixed pass ran its gates on the LDS kernel
+  // (C2 n = 28: one pass of 5 gate stages + 11 densities, 2.66 ms); split, the gates run
+  // register-resident and the densities join density-only passes (k_dens1)
+  bool split_dens = true;
 
   static uint32_t log2_of(uint64_t x) {
     uint32_t k = 0;
@@ -345,6 +350,7 @@ struct FusionPlanner {
           // is gates then densities (no gate after a density: its backward splits into the
           // injections, then the gates' mirrored stages)
           if ((backward && kind >= 0 && (int)meas != kind) || (mfwd && kind == 1 && !meas) ||
+              (!backward && split_dens && kind == 0 && meas) ||
               (q & blocked) ||
               (mfwd && meas && ndens + 1 > (uint32_t)FMAX_GRAD) ||
               (conflicts_of(cls) & left) || pass.size() >= fuse_max_ops ||

@@ -772,7 +772,27 @@ class SpecJit {
       disable("no private cache directory (" + why + ")");
       return false;
     }
-    fp = spec_fingerprint(spec_defines(), hipcc + "\n" + ver, sfp);
+    // the compiler's identity as the fingerprint sees it: its canonical path and the version
+    // lines of its --version text, so a run under a profiler (another ROCM_PATH spelling, a
+    // preloaded tool writing to the child's stdout) names the same kernels as a plain run
+    std::string ident;
+    {
+      char rbuf[4096];
+      ident = realpath(hipcc.c_str(), rbuf) ? std::string(rbuf) : hipcc;
+      size_t p0 = 0;
+      while (p0 < ver.size()) {
+        size_t p1 = ver.find('\n', p0);
+        if (p1 == std::string::npos) p1 = ver.size();
+        const std::string line = ver.substr(p0, p1 - p0);
+        for (const char* key : {"HIP version", "AMD clang version", "clang version", "Target:"})
+          if (line.rfind(key, 0) == 0) {
+            ident += "\n" + line;
+            break;
+          }
+        p0 = p1 + 1;
+      }
+    }
+    fp = spec_fingerprint(spec_defines(), ident, sfp);
     {
       const char* pe = getenv("QDC_JIT_PREBUILT");
       std::string p = pe ? std::string(pe) : libdir + "/../jit-prebuilt";

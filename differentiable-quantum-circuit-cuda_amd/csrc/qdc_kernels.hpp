@@ -1657,6 +1657,128 @@ void k_fused(chunk* __restrict__ f, chunk* __restrict__ b, const fop* __restrict
   }
 }
 
+// Read-only passes of one-qubit densities (round 6; the final densities of C2 / C5 and every
+// density-only pass of a forward).  k_fused<false, TB, true, false> reduces each density of a
+// tile on its own — a 64-lane reduce-scatter, an LDS accumulate and a block barrier per density
+// and tile — and ran such passes at 0.30 of HBM.  Here every thread keeps its densities'
+// partial sums in registers across all tiles of its block (rho11 and rho01 per density: the
+// power of bit t = 1 and the cross term; rho00 = the tile power - rho11), so a tile costs two
+// barriers and six FMAs per amplitude pair and density, and the block reduces once at the end.
+// Same tiles (lc, h, hb, gap) and partial slots as k_fused: densities in slot order 0..nops-1,
+// each partial [rho00, rho01, rho10, rho11, 0...] (rho_pq = sum f_p conj(f_q)).
+constexpr int DENS1_MAX = 16;  // densities of one pass (the planner's FMAX_GRAD)
+static_assert(DENS1_MAX <= FMAX_GRAD, "a density pass holds at most FMAX_GRAD densities");
+template <int TB, int NT>
+__global__ __launch_bounds__(NT) void k_dens1(const chunk* __restrict__ f, const fop* __restrict__ ops,
+                                              fgeo fg, cx* __restrict__ partials,
+                                              uint64_t slot_stride) {
+  constexpr int CPT = TB / NT;  // chunks per thread and tile
+  constexpr uint32_t ta = TB * VEC;  // amplitudes per tile
+  static_assert(TB % NT == 0 && ta >= 2 * NT, "tile must cover the block");
+  __shared__ chunk lds[TB];
+  __shared__ real red[NT / 64][3 * DENS1_MAX + 1];
+  const uint32_t t = threadIdx.x;
+  const cx* lf = reinterpret_cast<const cx*>(&lds[0]);
+  const uint32_t nops = fg.nops;  // <= DENS1_MAX (host)
+  uint64_t off[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const uint32_t c = t + (uint32_t)i * NT;
+    uint64_t o = c & ((1u << fg.lc) - 1u);
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) o += (uint64_t)((c >> (fg.lc + k)) & 1u) << fg.hb[k];
+    off[i] = o + (o & fg.gm);
+  }
+  auto tile_base = [&](uint64_t tile) {
+    uint64_t base = tile << fg.lc;
+#pragma unroll
+    for (int k = 0; k < FMAX_ROWS; ++k)
+      if ((uint32_t)k < fg.h) base = insert_zero(base, fg.hb[k]);
+    return base + (base & fg.gm);
+  };
+  real p11[DENS1_MAX], c01r[DENS1_MAX], c01i[DENS1_MAX], ptot = 0;
+#pragma unroll
+  for (int j = 0; j < DENS1_MAX; ++j) p11[j] = c01r[j] = c01i[j] = 0;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * fg.tpb;
+  const uint32_t count =
+      tile0 >= fg.ntiles ? 0u : (uint32_t)min<uint64_t>(fg.tpb, fg.ntiles - tile0);
+  chunk pf[CPT];
+  if (count) {
+    const uint64_t b0 = tile_base(tile0);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) pf[i] = ldc(f + b0 + off[i]);
+  }
+  for (uint32_t tt = 0; tt < count; ++tt) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      lds[swz_chunk(t + (uint32_t)i * NT)] = pf[i];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) ptot += pf[i].v[v].x * pf[i].v[v].x + pf[i].v[v].y * pf[i].v[v].y;
+    }
+    __syncthreads();
+    if (tt + 1 < count) {  // the next tile in flight while this one is reduced
+      const uint64_t nb = tile_base(tile0 + tt + 1);
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) pf[i] = ldc(f + nb + off[i]);
+    }
+    // (guarded, not broken out of: the loop unrolls, so the accumulators stay in registers)
+#pragma unroll
+    for (int j = 0; j < DENS1_MAX; ++j) {
+      if ((uint32_t)j < nops) {
+        const uint32_t t1 = ops[j].t1;
+        const uint32_t s1 = swz(1u << t1);
+        const uint32_t abase = swz((uint32_t)insert_zero(t, t1));
+#pragma unroll
+        for (uint32_t it = 0; it < ta / (2 * NT); ++it) {
+          const uint32_t a0 = abase ^ swz((uint32_t)insert_zero(it * NT, t1));
+          const cx x0 = lf[a0], x1 = lf[a0 ^ s1];
+          p11[j] = fma(x1.x, x1.x, fma(x1.y, x1.y, p11[j]));
+          c01r[j] = fma(x0.x, x1.x, fma(x0.y, x1.y, c01r[j]));
+          c01i[j] = fma(x0.y, x1.x, fma(-x0.x, x1.y, c01i[j]));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // block reduction: 64-lane sums, then the waves' sums per value
+  const int lane = t & 63, wave = t >> 6;
+  auto wsum = [&](real x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+  };
+  {
+    const real s = wsum(ptot);
+    if (lane == 0) red[wave][3 * DENS1_MAX] = s;
+  }
+#pragma unroll
+  for (int j = 0; j < DENS1_MAX; ++j) {
+    if ((uint32_t)j < nops) {
+      const real a = wsum(p11[j]), b = wsum(c01r[j]), c = wsum(c01i[j]);
+      if (lane == 0) {
+        red[wave][3 * j] = a;
+        red[wave][3 * j + 1] = b;
+        red[wave][3 * j + 2] = c;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < nops * RED; i += NT) {
+    const uint32_t k = i / RED, e = i % RED;
+    real pw = 0, a = 0, b = 0, c = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+      pw += red[w][3 * DENS1_MAX];
+      a += red[w][3 * k];
+      b += red[w][3 * k + 1];
+      c += red[w][3 * k + 2];
+    }
+    const cx v = e == 0 ? cx{pw - a, 0} : e == 1 ? cx{b, c} : e == 2 ? cx{b, -c} : e == 3 ? cx{a, 0} : cx{0, 0};
+    partials[(uint64_t)k * slot_stride + (uint64_t)blockIdx.x * RED + e] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Remap pack (qdc_shard.hpp): dst block j (victim bit pattern j) = the source chunks whose
 // victim bits equal j, in order.  dst[o] = src[expand(o)]: insert zeros at the victim chunk

@@ -491,3 +491,36 @@ def test_diagonal_injections_equal_general(prec, case):
         assert ("inject_diag" in stats) == (mode == "1"), sorted(stats)
         out[mode] = g
     F.check_pair(prec, out["1"], out["0"], fl.floor["grads"], f"diag-inject {case} {prec} on vs off grads")
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("n", [16, 20])
+def test_density_only_passes_and_split(monkeypatch, prec, n):
+    """Round 6: forward passes hold gates or densities, not both (QDC_DENS_SPLIT), so the last
+    gates stay register-resident, and density-only passes of one-qubit densities run on k_dens1
+    (QDC_DENS1: register partial sums across a block's tiles) — against the floors, and against
+    the round-5 schedule (mixed passes, k_fused's per-tile reductions) within 8x the floor; with
+    q1 and q2 densities mid-circuit too (mixed-kind density passes stay on k_fused)."""
+    ins, var = O.layered_circuit(n, 3, seed=11)
+    cut = len(ins) // 2
+    ins = ins[:cut] + [(O.DIFF_Q1_DENSITY, (q,)) for q in (0, 5, n - 1)] + \
+        [(O.DIFF_Q2_DENSITY, (n - 2, 3))] + ins[cut:]
+    fl = F.Floor(prec, n, ins, [], var, run=False)
+    res = {}
+    for new in (False, True):
+        for k in ("QDC_DENS_SPLIT", "QDC_DENS1"):
+            if new:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, "0")
+        c = build(prec, n, ins, 1)
+        c.profile(True)
+        what = f"density passes n={n} {prec} {'split + k_dens1' if new else 'round 5'} "
+        d = c.forward([], fl.var)
+        g = c.backward(fl.cots, [], fl.var)
+        fl.check("forward", d, what)
+        fl.check("grads", g, what)
+        res[new] = (d, g, c.profile_collect())
+    F.check_pair(prec, res[True][0], res[False][0], fl.floor["forward"], f"n={n} {prec} densities new vs round 5")
+    F.check_pair(prec, res[True][1], res[False][1], fl.floor["grads"], f"n={n} {prec} grads new vs round 5")
+    assert res[True][2]["fused_density"]["launches"] >= 1, sorted(res[True][2])

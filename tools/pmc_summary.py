@@ -45,6 +45,8 @@ def bench_name(kernel):
     m = re.search(r"k_r[qw]<(true|false), \d+[^>]*>", kernel)
     if m:  # register-resident gate passes (qdc_rq.hpp): k_rq<TWO, NT, PF>, k_rw<TWO, NE, PF>
         return "fused_reverse" if m.group(1) == "true" else "fused_apply"
+    if "k_dens1<" in kernel:  # read-only one-qubit density passes (round 6)
+        return "fused_density"
     if "k_elementwise<0>" in kernel:
         return "copy"
     if "k_elementwise<4>" in kernel:
