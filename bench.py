@@ -669,6 +669,19 @@ def main():
             c.synchronize()
     warmup_s = time.perf_counter() - tw  # includes the specialized kernels' compilation
 
+    # QDC_BENCH_UNPROFILED_STEPS=K (experiment): K more timed steps without the per-launch HIP
+    # events first, reported as unprofiled_ms_per_step (what the events cost the step)
+    unprof = int(os.environ.get("QDC_BENCH_UNPROFILED_STEPS", "0"))
+    unprof_ms = None
+    if unprof > 0:
+        barrier(comm)
+        c.synchronize()
+        tu = time.perf_counter()
+        for _ in range(unprof):
+            c.forward([], vg)
+            c.backward(cots, [], vg)
+        c.synchronize()
+        unprof_ms = max_over_ranks(time.perf_counter() - tu, comm) / unprof * 1e3
     c.profile(True)
     c.host_times(reset=True)
     barrier(comm)
@@ -865,6 +878,7 @@ def main():
             "vqse_c3": vqse,
             "vqse_c3_f32": vqse32,
             "exchange": exchange,
+            "unprofiled_ms_per_step": round(unprof_ms, 3) if unprof_ms else None,
             "abi_unfused": abi,
             "cpu_baseline": cpu,
         }
