@@ -75,6 +75,7 @@ QDC_API const char* qdc_circuit_set_state_from_vector(qdc_circuit* c, const qdc_
   if (len != ((size_t)1 << k.n))
     return qdc::fail("Size of the given state does not match the size of the tensor.");
   const size_t shard = (size_t)1 << k.nl;
+  k.initial_standard = false;
   for (size_t s = 0; s < k.sh.size(); ++s) {
     QDC_TRY(k.sh[s].c().use());
     QDC_HIP(hipMemcpyAsync(k.sh[s].initial, vec + (size_t)(k.ex.rank0 + s) * shard,

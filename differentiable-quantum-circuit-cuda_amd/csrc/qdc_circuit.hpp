@@ -535,7 +535,18 @@ struct Circuit {
     return nullptr;
   }
   // (kernels: a 2-D hipMemset / hipMemcpy over the 64 KiB blocks runs at < 1 TB/s)
-  const char* copy_initial(Shard& s) { return elementwise<0>(s.c(), s.initial, s.state, nl, gm); }
+  // every call starts from `initial`; while that is the standard state (the reference's
+  // new_standard, circuit.rs:96-102: no set_state_from_vector yet) the state is written directly
+  // (|0..0> on shard 0, zeros elsewhere: one write of S instead of a copy's read and write)
+  bool initial_standard = true;
+  const char* copy_initial(Shard& s) {
+    if (initial_standard) {
+      const bool first = ex.rank0 + (int)(&s - sh.data()) == 0;
+      return first ? elementwise<3>(s.c(), nullptr, s.state, nl, gm)
+                   : elementwise<4>(s.c(), nullptr, s.state, nl, gm);
+    }
+    return elementwise<0>(s.c(), s.initial, s.state, nl, gm);
+  }
   const char* zero_bwd(Shard& s) {
     if (gm) return elementwise<4>(s.c(), nullptr, s.bwd, nl, gm);
     QDC_HIP(hipMemsetAsync(s.bwd, 0, ((size_t)1 << nl) * sizeof(cx), s.c().stream));

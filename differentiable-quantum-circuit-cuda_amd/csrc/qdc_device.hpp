@@ -70,11 +70,16 @@ struct Prof {
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<ProfRecord> recs;
+  // Timing-only events: no system-scope fence when an event is recorded (a default event writes
+  // back and invalidates the caches at every record, i.e. twice per profiled launch, and the
+  // next kernel starts cold).  The records are read only after the stream is synchronised.
+  // QDC_EVENT_FENCE=1 restores default events.
+  unsigned flags = hipEventDisableSystemFence;
 
   hipEvent_t get() {
     if (used == pool.size()) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
       pool.push_back(e);
     }
     return pool[used++];
@@ -136,7 +141,8 @@ struct Ctx {
   // XCD-aware block order of streaming single-gate launches (direct and tile families; knob
   // QDC_XCD_MAP): the blocks one XCD runs own adjacent ranges.  Measured at n = 28
   // (profiles/r2t_micro_table_xcd*.txt): injections at q1 1..6 71 -> 76 %, apply/inject at
-  // q1 7..11 and 21..23 +4..7 points, apply_q2 71.6 -> 73.4 %; q1 24 71.8 -> 69.4 %
+  // q1 7..11 and 21..23 +4..7 points, apply_q2 71.6 -> 73.4 %; q1 24 71.8 -> 69.4 %.
+  // Bits: 0 streaming launches, 1 reducing launches, 2 diagonal launches (k_diag, round 6)
   uint32_t xcd_map = 1;
   // two-state tile-family launches on 2^10-chunk tiles (K = 4, 32 KiB of LDS per block) instead
   // of 2^9 (knob QDC_TILE2_WIDE): longer rows per far row bit.  Measured at n = 28
@@ -180,6 +186,10 @@ struct Ctx {
   unsigned long long* dctr = nullptr;  // 8 dynamic-tail counters (plan_dyn)
   uint64_t dbase = 0;
   uint32_t dyn_static_pct = 35;  // QDC_DYN: static share of the fair share, % (100: off)
+  // smallest granule (tiles per grab) of a reducing dynamic tail (QDC_DYN_GRAN, a power of two
+  // <= 32): every granule writes its own partial per reduction slot, which k_dsum pre-sums —
+  // C2's reverse passes at granule 2: ~43 000 partials per Gamma slot, ~0.35 GB per flush
+  uint32_t dyn_gran_min = 1;
   // granule partials of dynamic-tail passes: [FIN_MAX][DYN_CAP][RED], slot i beside partials'
   cx* dparts = nullptr;
   cx* dsums = nullptr;  // [FIN_MAX][DYN_CAP / BLOCK][RED]: k_dsum's chunk sums
@@ -197,6 +207,12 @@ struct Ctx {
     QDC_HIP(hipMalloc(&dctr, sizeof(unsigned long long) * 8 * FG_DCTR_STRIDE));
     QDC_TRY(dyn_reset());
     if (const char* e = getenv("QDC_DYN")) dyn_static_pct = (uint32_t)std::max(0, atoi(e));
+    if (const char* e = getenv("QDC_DYN_GRAN")) {
+      const int v = atoi(e);
+      dyn_gran_min = (v >= 1 && v <= 32 && (v & (v - 1)) == 0) ? (uint32_t)v : 1u;
+    }
+    if (const char* e = getenv("QDC_EVENT_FENCE"))
+      prof.flags = atoi(e) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
     if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
@@ -259,7 +275,7 @@ struct Ctx {
     }
     uint64_t per = g.ntiles * dyn_static_pct / 100 / grid;
     uint64_t ndyn = g.ntiles - per * grid;  // a multiple of 8 (ntiles and grid are)
-    uint32_t gran = 1;
+    uint32_t gran = g.ngrad > 0 ? dyn_gran_min : 1u;
     if (g.ngrad > 0)
       while (ndyn / gran > DYN_CAP || (ndyn % (8ull * gran)) != 0) {
         if (gran >= 64) return false;
@@ -271,7 +287,7 @@ struct Ctx {
           per += add;
           if (per * grid > g.ntiles) return false;
           ndyn = g.ntiles - per * grid;
-          gran = 1;  // re-check from the smallest granule with the new split
+          gran = dyn_gran_min;  // re-check from the smallest granule with the new split
         }
       }
     if (ndyn == 0) return false;
@@ -807,6 +823,7 @@ inline dgeo diag_geo(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, uin
   if (target == c.grid_cap && g.it < c.direct_it) g.it = c.direct_it;  // streaming
   g.p2 = pos2;
   g.p1 = pos1;
+  g.xcd = (c.xcd_map >> 2) & 1u;  // QDC_XCD_MAP bit 2: diagonal launches
   return g;
 }
 inline uint32_t diag_blocks(const dgeo& g) {

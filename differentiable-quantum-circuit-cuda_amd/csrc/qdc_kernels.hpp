@@ -824,6 +824,7 @@ struct dgeo {
   uint32_t it;
   uint32_t p2, p1;
   uint64_t gm;  // gap mask (geo::gm)
+  uint32_t xcd;  // XCD-aware block order (the blocks of one XCD own adjacent ranges)
 };
 
 template <int OP, int U>
@@ -833,7 +834,8 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
   constexpr bool RED_ = (OP == DIAG_REVERSE_GRAD || OP == DIAG_GRAD);
   constexpr bool TWO = (OP != DIAG_APPLY);
   cx acc[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-  const uint64_t start = (uint64_t)blockIdx.x * BLOCK * g.it + threadIdx.x;
+  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, g.xcd);
+  const uint64_t start = (uint64_t)blk * BLOCK * g.it + threadIdx.x;
   auto body = [&](auto guarded) __attribute__((always_inline)) {  // as k_direct
   for (uint32_t step = 0; step < g.it; step += U) {
     chunk fc[U], bc[U];
@@ -878,7 +880,7 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
     }
   }
   };
-  if ((uint64_t)(blockIdx.x + 1) * BLOCK * g.it <= g.nchunks && g.it % U == 0)
+  if ((uint64_t)(blk + 1) * BLOCK * g.it <= g.nchunks && g.it % U == 0)
     body(std::false_type{});
   else
     body(std::true_type{});
