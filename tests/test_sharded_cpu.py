@@ -1,4 +1,4 @@
-"""The sharded-state path on CPU ranks (gloo, world size 2 and 4).
+"""The sharded-state path on CPU ranks (gloo, world size 2, 4 and 8).
 
 Each rank executes the native planner's plans (qdc_plan, the same code the HIP runtime runs)
 on a numpy shard of 2^(n-g) amplitudes: ops at the planned physical positions with the
@@ -213,12 +213,16 @@ def make_case(case):
     return n, ins, [], var, psi0, sz_cots
 
 
-@pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("case", ["autodiff", "layered", "autodiff_mirror", "layered_mirror"])
+CASES = ["autodiff", "layered", "autodiff_mirror", "layered_mirror"]
+
+
+@pytest.mark.parametrize("world,case", [(w, c) for w in (2, 4) for c in CASES] +
+                         [(8, "autodiff_mirror"), (8, "layered_mirror")])
 def test_sharded_plan_execution_matches_oracle(world, case):
     """`*_mirror`: the mirrored forward plan (qdc_plan mode 3) and, as the backward, that plan
     reversed with every remap undone (all-to-all, then the inverse pack) — the schedule of the
-    runtime's mirrored reverse sweeps on sharded circuits."""
+    runtime's mirrored reverse sweeps on sharded circuits.  World 8: the 8-GPU configuration's
+    rank count (three rank bits, gloo ranks on CPU), in the mirrored schedule the runtime runs."""
     ctx = mp.get_context("spawn")
     q_out = ctx.Queue()
     port = free_port()
