@@ -120,6 +120,10 @@ struct Ctx {
   hipStream_t stream = nullptr;
   uint32_t grid_cap = 1u << 20;  // streaming launches: ~one item per thread (measured best)
   uint32_t red_cap = 2048;   // target blocks of reduction launches (<= NBMAX)
+  // the same for the single-gate reverse with its gradient (both states read and written; knob
+  // QDC_REV_RED): at 4096 instead of 2048 blocks reverse_q2 +1..2 points at 5 of 7 pairs
+  // ((26,27) 72.4 -> 74.3 %, (0,1) 75.9 -> 77.1 %), reverse_q1 +0.5..1 (profiles/r6/r6m)
+  uint32_t rev_red_cap = NBMAX;
   double next_flops = 0;     // algorithmic FLOPs of the next launch (profiling; reset by launch)
   // gap mask of the states this context's gate-shaped launches address: chunk c of a state at
   // c + (c & gm).  Nonzero for a circuit whose fwd / bwd states are interleaved in one
@@ -165,9 +169,21 @@ struct Ctx {
   // 1, 4 or 8)
   uint32_t lane_u[3] = {8, 1, 4};
   // chunks per state in flight per thread and step of the diagonal reverse kernels (knob
-  // QDC_DIAG_RU: 2 or 8; 8 = a block's step moves 32 KiB of each state, as the tile family):
-  // reverse_q2_diag 71.4 -> 73.3 % (profiles/r5/r5l_*)
-  uint32_t diag_ru = 8;
+  // QDC_DIAG_RU: 4, 8 or 16; k_diag takes 2 or 8; 8 = a block's step moves 32 KiB of each state,
+  // as the tile family): k_diag reverse_q2_diag 71.4 -> 73.3 % (profiles/r5/r5l_*); k_diag_q
+  // 74.5 / 75.4 / 76.7 % at 4 / 8 / 16 (profiles/r6/r6l)
+  uint32_t diag_ru = 16;
+  // target blocks of the diagonal reverse's reducing launches (knob QDC_DIAG_RED, <= NBMAX):
+  // k_diag_q with 16 in flight 76.7 -> 77.3 % at 2048 -> 4096 blocks (profiles/r6/r6l)
+  uint32_t diag_red = NBMAX;
+  // diagonal reverse launches on k_diag_q (k and the matrix entries fixed per thread; knob
+  // QDC_DIAG_Q = 0: k_diag)
+  uint32_t diag_q = 1;
+  // tile-family blocks of several tiles (reducing launches) load the next tile during this
+  // tile's math (knob QDC_TILE_PF), on tiles without far row bits: reverse_q2 (0,1) / (1,2)
+  // +0.7..1.0 points; with row bits it measured 2.5-3 points slower (reverse_q1 at 12..27,
+  // reverse_q2 (5,20), (27,0); profiles/r6/r6m)
+  uint32_t tile_pf = 1;
   // streaming LANE launches with a target beyond the wave's chunk bits on the block-wide
   // variant (k_lane_blk; knob QDC_LANE_BLK): +1..3.5 points at 13 of 27 far placements, -1..4
   // at 5 (profiles/r5/r5m_*, r5n_*); the far-row cells that stay near 71 % (q1 20, 24) do so
@@ -215,6 +231,7 @@ struct Ctx {
       prof.flags = atoi(e) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
     if (const char* e = getenv("QDC_GRID_CAP")) grid_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RED_CAP")) red_cap = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_REV_RED")) rev_red_cap = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIRECT_IT")) direct_it = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE_FAR")) tile_far = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_XCD_MAP")) xcd_map = (uint32_t)atoi(e);
@@ -222,6 +239,9 @@ struct Ctx {
     if (const char* e = getenv("QDC_TILE1_WIDE")) tile1_wide = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_LANE")) lane_ops = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_DIAG_RU")) diag_ru = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_DIAG_Q")) diag_q = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_DIAG_RED")) diag_red = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_TILE_PF")) tile_pf = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_LANE_BLK")) lane_blk = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_LANE_U")) {
       unsigned u0 = 0, u1 = 0, u2 = 0;
@@ -234,6 +254,8 @@ struct Ctx {
     if (grid_cap < 1) grid_cap = 1;
     if (red_cap < 1) red_cap = 1;
     if (red_cap > NBMAX) red_cap = NBMAX;
+    rev_red_cap = std::max(1u, std::min(rev_red_cap, NBMAX));
+    diag_red = std::max(1u, std::min(diag_red, NBMAX));
     return nullptr;
   }
   // make this context's device current (launches and allocations of a shard go to its device)
@@ -789,9 +811,10 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   const uint32_t cls = writes_both ? 0u : two ? 2u : 1u;  // QDC_TILE_FAR bit
   Plan p;
   const uint32_t lcls = writes_both ? 0u : reduces ? 2u : 1u;  // QDC_LANE bit
+  const uint32_t rcap = writes_both ? c.rev_red_cap : c.red_cap;
   if (!((c.lane_ops >> lcls) & 1u) ||
-      !plan_lane(n, R, pos2, pos1, c.red_cap, reduces, p, c.lane_u[lcls])) {
-    p = plan_gate(n, R, pos2, pos1, two, reduces ? c.red_cap : c.grid_cap,
+      !plan_lane(n, R, pos2, pos1, rcap, reduces, p, c.lane_u[lcls])) {
+    p = plan_gate(n, R, pos2, pos1, two, reduces ? rcap : c.grid_cap,
                   (c.tile_far >> cls) & 1u, c.tile2_wide, c.tile1_wide);
     if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
   } else if (lcls == 1 && c.lane_blk && p.lg.nf > 0) {
@@ -804,6 +827,7 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   p.g.xcd = p.tg.xcd = p.lg.xcd = (c.xcd_map >> (reduces ? 1 : 0)) & 1u;  // bit 0 streaming, 1 reducing
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
+  p.tg.pf = c.tile_pf && p.tg.h == 0;
   p.lg.gm = c.gm;
   return p;
 }
@@ -828,6 +852,37 @@ inline dgeo diag_geo(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, uin
 }
 inline uint32_t diag_blocks(const dgeo& g) {
   return (uint32_t)((g.nchunks + (uint64_t)BLOCK * g.it - 1) / ((uint64_t)BLOCK * g.it));
+}
+// k_diag_q's geometry (qdc_kernels.hpp): false when the state does not split into whole
+// blocks of one quadrant each (small states), or when it is not a multiple of the kernel's U
+// chunks in flight — k_diag runs those
+inline bool diag_q_geo(const dgeo& g, dqgeo& q, uint32_t U) {
+  if (g.nchunks == 0 || (g.nchunks & (g.nchunks - 1)) != 0 || g.it % U != 0) return false;
+  uint32_t lognc = 0;
+  while (((uint64_t)1 << lognc) < g.nchunks) ++lognc;
+  q = dqgeo{};
+  q.gm = g.gm;
+  q.it = g.it;
+  uint32_t cb[2], nb = 0;
+  auto enc = [&](uint32_t p) -> uint32_t {
+    if (p < (uint32_t)LV) return 0x100u;
+    const uint32_t c = p - (uint32_t)LV;
+    if (c < 8) return 0x200u | c;
+    cb[nb++] = c;
+    return 0x400u | c;  // quadrant bit resolved below
+  };
+  q.k1 = enc(g.p1);
+  q.k2 = enc(g.p2);
+  if (nb == 2 && cb[0] > cb[1]) std::swap(cb[0], cb[1]);
+  for (uint32_t* k : {&q.k1, &q.k2})
+    if (*k & 0x400u) *k = 0x400u | ((*k & 0xffu) == cb[0] ? 0u : 1u);
+  q.nb = nb;
+  q.c0 = nb >= 1 ? cb[0] : 0;
+  q.c1 = nb >= 2 ? cb[1] : 0;
+  if (lognc < nb) return false;
+  q.qshift = lognc - nb;
+  const uint64_t span = (uint64_t)BLOCK * g.it;  // chunks per block
+  return span <= ((uint64_t)1 << q.qshift) && g.nchunks % span == 0;
 }
 
 inline const char* apply_diag(Ctx& c, cx* s, const diag4& d, uint32_t pos2, uint32_t pos1,
@@ -905,6 +960,25 @@ inline const char* reverse_diag(Ctx& c, cx* f, cx* b, const diag4& d, uint32_t p
   chunk* bc = reinterpret_cast<chunk*>(b);
   const diag4 dc = conj_diag(d);
   const double bytes = 4.0 * state_bytes(n);
+  if (c.diag_q) {  // k fixed per thread (k_diag_q), when the state splits into whole blocks
+    const uint32_t U = c.diag_ru >= 16 ? 16u : c.diag_ru >= 8 ? 8u : 4u;
+    dgeo g = diag_geo(c, n, pos2, pos1, grad_base ? c.diag_red : c.grid_cap);
+    g.it = std::max(g.it, U);
+    dqgeo q;
+    if (diag_q_geo(g, q, U)) {
+      const uint32_t nb = diag_blocks(g);
+      auto go = [&](auto kern, cx* out) { return c.launch("reverse_q2_diag", bytes, kern, nb, fc, bc, dc, d, q, out); };
+      if (grad_base)
+        return reduce_into(c, grad_base, dst, 0, nb, [&](cx* out) {
+          return U == 16 ? go(k_diag_q<DIAG_REVERSE_GRAD, 16>, out)
+                 : U == 8 ? go(k_diag_q<DIAG_REVERSE_GRAD, 8>, out)
+                          : go(k_diag_q<DIAG_REVERSE_GRAD, 4>, out);
+        });
+      return U == 16 ? go(k_diag_q<DIAG_REVERSE, 16>, nullptr)
+             : U == 8 ? go(k_diag_q<DIAG_REVERSE, 8>, nullptr)
+                      : go(k_diag_q<DIAG_REVERSE, 4>, nullptr);
+    }
+  }
   if (grad_base) {
     const dgeo g = diag_geo(c, n, pos2, pos1, c.red_cap);
     return reduce_into(c, grad_base, dst, 0, diag_blocks(g), [&](cx* out) {

@@ -384,6 +384,7 @@ struct tgeo {
   uint32_t t1, t2;    // tile-local amplitude bits of the gate's index bits 0 (pos1) and 1 (pos2)
   uint32_t xcd;       // XCD-aware block order (geo::xcd)
   uint64_t gm;        // gap mask (geo::gm)
+  uint32_t pf;        // the next tile's loads in flight during this tile's math (round 6)
 };
 
 __device__ __forceinline__ uint64_t tile_base(const tgeo& tg, uint64_t tile) {
@@ -416,19 +417,35 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
   const uint32_t lo_t = tg.t1 < tg.t2 ? tg.t1 : tg.t2;
   const uint32_t hi_t = tg.t1 < tg.t2 ? tg.t2 : tg.t1;
   const uint64_t tile0 = (uint64_t)xcd_block(blockIdx.x, gridDim.x, tg.xcd) * tg.tpb;
-  for (uint32_t tt = 0; tt < tg.tpb; ++tt) {
-    const uint64_t tile = tile0 + tt;
-    if (tile >= tg.ntiles) break;
+  // A block's tiles are software-pipelined (round 6): the next tile's loads are issued into
+  // registers before this tile's gate math on LDS and its stores, so a block with several
+  // tiles (the reducing launches: tpb = 16-32) keeps its loads in flight through the compute
+  // phase.  (Streaming launches run one tile per block.)
+  uint64_t gi[K];
+  chunk rf[K], rb[K];
+  auto load = [&](uint64_t tile) __attribute__((always_inline)) {
     const uint64_t base = tile_base(tg, tile);
-    uint64_t gi[K];
-    chunk rf[K], rb[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (k * BLOCK + t >= tc) break;
-      gi[k] = tile_chunk(tg, base, k * BLOCK + t);
-      gi[k] += gi[k] & tg.gm;
-      rf[k] = ldc(f + gi[k]);
-      if constexpr (op_reads_b(OP)) rb[k] = ldc(b + gi[k]);
+      uint64_t g = tile_chunk(tg, base, k * BLOCK + t);
+      g += g & tg.gm;
+      rf[k] = ldc(f + g);
+      if constexpr (op_reads_b(OP)) rb[k] = ldc(b + g);
+    }
+  };
+  if (tile0 < tg.ntiles) load(tile0);
+  for (uint32_t tt = 0; tt < tg.tpb; ++tt) {
+    const uint64_t tile = tile0 + tt;
+    if (tile >= tg.ntiles) break;
+    {
+      const uint64_t base = tile_base(tg, tile);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (k * BLOCK + t >= tc) break;
+        gi[k] = tile_chunk(tg, base, k * BLOCK + t);
+        gi[k] += gi[k] & tg.gm;
+      }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -437,6 +454,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
       if constexpr (op_reads_b(OP)) lds[NS - 1][k * BLOCK + t] = rb[k];
     }
     __syncthreads();
+    if (tg.pf && tt + 1 < tg.tpb && tile + 1 < tg.ntiles) load(tile + 1);
     cx* lf = reinterpret_cast<cx*>(&lds[0][0]);
     cx* lb = reinterpret_cast<cx*>(&lds[NS - 1][0]);
     for (uint32_t grp = t; grp < ng; grp += BLOCK) {
@@ -476,6 +494,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile(chunk* __restrict__ f, chunk* __
       }
     }
     __syncthreads();  // the next tile overwrites lds
+    if (!tg.pf && tt + 1 < tg.tpb && tile + 1 < tg.ntiles) load(tile + 1);
   }
   if constexpr (op_reduces(OP)) block_reduce_store<NACC>(acc, partials + (uint64_t)blockIdx.x * RED);
 }
@@ -885,6 +904,101 @@ __global__ __launch_bounds__(BLOCK) void k_diag(chunk* __restrict__ f, chunk* __
   else
     body(std::true_type{});
   if constexpr (RED_) block_reduce_store<4>(acc, partials + (uint64_t)blockIdx.x * RED);
+}
+
+// Diagonal two-qubit gates with the diagonal index k fixed per thread and amplitude slot
+// (round 6; knob QDC_DIAG_Q).  A gate position is the in-chunk amplitude bit (f32 qubit 0), a
+// "thread" chunk bit (< 8: the thread index supplies it) or a "block" chunk bit (>= 8).  Blocks
+// walk the state by quadrant: the block bits of chunk i are the top bits of the iteration index
+// j, so every block sees one value of them and chunk i = D(j - t) + t with D the bit deposit
+// (uniform).  k, the two matrix entries and the accumulator of each amplitude slot are then
+// constants of the thread — per amplitude the pass costs its three complex multiplies and
+// nothing else (k_diag selects entries and accumulators per amplitude).  Runs of >= 256
+// contiguous chunks, as k_diag.  Host: diag_q_geo (qdc_device.hpp).  Measured at n = 28 f32
+// (profiles/r6/r6k, r6l): reverse_q2_diag 73.1 % (k_diag) -> 75.4 % at 8 chunks in flight per
+// state, 76.7 % at 16, 77.3 % at 16 with 4096 blocks (the default).
+struct dqgeo {
+  uint64_t gm;        // gap mask (geo::gm)
+  uint32_t it;        // chunks per thread (a multiple of U)
+  uint32_t qshift;    // j bit where the quadrant index starts (log2 nchunks - nb)
+  uint32_t c0, c1;    // block chunk bits, ascending (nb of them are valid)
+  uint32_t nb;        // 0, 1 or 2
+  // where the k bit of pos1 / pos2 comes from: 0x100 the amplitude slot v, 0x200 | s thread
+  // bit s, 0x400 | q bit q of the block's quadrant index
+  uint32_t k1, k2;
+};
+
+template <int OP, int U>
+__global__ __launch_bounds__(BLOCK) void k_diag_q(chunk* __restrict__ f, chunk* __restrict__ b,
+                                                  diag4 dc, diag4 d, dqgeo g,
+                                                  cx* __restrict__ partials) {
+  constexpr bool RED_ = (OP == DIAG_REVERSE_GRAD || OP == DIAG_GRAD);
+  constexpr bool TWO = (OP != DIAG_APPLY);
+  const uint32_t t = threadIdx.x;
+  const uint64_t jb = (uint64_t)blockIdx.x * BLOCK * g.it;
+  const uint32_t qd = (uint32_t)(jb >> g.qshift);  // this block's quadrant
+  uint32_t k[VEC];  // k = 2 bit(pos2) + bit(pos1) per amplitude slot
+  auto kbit = [&](uint32_t enc, int v) -> uint32_t {
+    if (enc & 0x100u) return (uint32_t)v & 1u;
+    if (enc & 0x200u) return (t >> (enc & 0xffu)) & 1u;
+    return (qd >> (enc & 0xffu)) & 1u;
+  };
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) k[v] = (kbit(g.k2, v) << 1) | kbit(g.k1, v);
+  cx ca[VEC], cb[VEC], acc[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    ca[v] = pick4(OP == DIAG_APPLY ? d : dc, k[v]);
+    cb[v] = pick4(d, k[v]);
+    acc[v] = {0, 0};
+  }
+  // D(j - t): the block bits deposited at c0 (< c1), from the quadrant index
+  const uint64_t jmask = ((uint64_t)1 << g.qshift) - 1;
+  auto deposit = [&](uint64_t j) -> uint64_t {
+    uint64_t x = j & jmask;
+    if (g.nb >= 1) x = insert_zero(x, g.c0) | ((uint64_t)(qd & 1u) << g.c0);
+    if (g.nb >= 2) x = insert_zero(x, g.c1) | ((uint64_t)((qd >> 1) & 1u) << g.c1);
+    return x;
+  };
+  for (uint32_t step = 0; step < g.it; step += U) {
+    chunk fc[U], bc[U];
+    uint64_t a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = deposit(jb + (uint64_t)(step + u) * BLOCK) + t;
+      a[u] = i + (i & g.gm);
+      fc[u] = ldc(f + a[u]);
+      if constexpr (TWO) bc[u] = ldc(b + a[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        if constexpr (OP == DIAG_APPLY) {
+          fc[u].v[v] = cmul(ca[v], fc[u].v[v]);
+        } else if constexpr (OP == DIAG_GRAD) {
+          acc[v] = cfma(bc[u].v[v], fc[u].v[v], acc[v]);
+        } else {
+          const cx fv = cmul(ca[v], fc[u].v[v]);
+          if constexpr (OP == DIAG_REVERSE_GRAD) acc[v] = cfma(bc[u].v[v], fv, acc[v]);
+          fc[u].v[v] = fv;
+          bc[u].v[v] = cmul(cb[v], bc[u].v[v]);
+        }
+      }
+      if constexpr (OP != DIAG_GRAD) stc(f + a[u], fc[u]);
+      if constexpr (OP == DIAG_REVERSE || OP == DIAG_REVERSE_GRAD) stc(b + a[u], bc[u]);
+    }
+  }
+  if constexpr (RED_) {
+    cx acc4[4];
+#pragma unroll
+    for (uint32_t kk = 0; kk < 4; ++kk) {
+      acc4[kk] = {0, 0};
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc4[kk] = cadd(acc4[kk], (k[v] == kk) ? acc[v] : cx{0, 0});
+    }
+    block_reduce_store<4>(acc4, partials + (uint64_t)blockIdx.x * RED);
+  }
 }
 
 // ---------------------------------------------------------------------------------------

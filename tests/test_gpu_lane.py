@@ -80,10 +80,11 @@ def _placement_failures(prec, n):
     return bad
 
 
-def _reverse_failures(prec, n):
+def _reverse_failures(prec, n, diag_only=False):
     """The runtime's single-gate reverse kernels (uncompute + gradient + pull-back, fusion off)
-    at every q1 position and ordered q2 pair (dense and diagonal): gradients and the uncomputed
-    state against the oracle's circuit (src/circuit.rs:266-429)."""
+    at every q1 position and ordered q2 pair (dense and diagonal; diag_only: a q1 layer and the
+    diagonal pairs): gradients and the uncomputed state against the oracle's circuit
+    (src/circuit.rs:266-429)."""
     import quantum_differentiable_circuit as q
     rng = np.random.default_rng(7 + n)
     ins, var = [], []
@@ -93,8 +94,11 @@ def _reverse_failures(prec, n):
     for pos2 in range(n):
         for pos1 in range(n):
             if pos2 != pos1:
-                ins += [(O.VAR_Q2, (pos2, pos1)), (O.VAR_Q2_DIAG, (pos2, pos1))]
-                var += [O.haar_unitary(rng, 4), np.exp(1j * rng.standard_normal(4))]
+                if not diag_only:
+                    ins.append((O.VAR_Q2, (pos2, pos1)))
+                    var.append(O.haar_unitary(rng, 4))
+                ins.append((O.VAR_Q2_DIAG, (pos2, pos1)))
+                var.append(np.exp(1j * rng.standard_normal(4)))
     ins += [(O.DIFF_Q1_DENSITY, (p,)) for p in range(n)]
     vg = [np.ascontiguousarray(g, dtype=DT[prec]) for g in var]
     c = q.circuit_class(prec)(n)
@@ -148,3 +152,16 @@ def test_lane_every_op_class(prec):
     bad = json.loads(r.stdout.strip().splitlines()[-1])
     print(f"[lane] QDC_LANE=7 {prec}: {len(bad)} failing cells")
     assert not bad, f"{len(bad)} failing cells: " + "; ".join(bad[:40])
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("n", [14, 16])
+def test_diag_reverse_every_pair(prec, n, monkeypatch):
+    """The diagonal reverse kernel with k fixed per thread (k_diag_q, qdc_kernels.hpp): at n = 14
+    and 16 the state splits into whole blocks per quadrant, so every ordered pair runs on it —
+    positions at the in-chunk amplitude bit, at thread chunk bits (< 8) and at block chunk bits
+    (one or both: quadrant walks) — uncompute, gradient and pull-back against the oracle's
+    circuit, fusion off (primitives.cu:649-672 via circuit.rs:320-392)."""
+    monkeypatch.setenv("QDC_FUSE", "0")
+    bad = _reverse_failures(prec, n, diag_only=True)
+    assert not bad, "; ".join(bad)
