@@ -825,6 +825,11 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   // XCD-aware order for streaming launches only by default: reductions (few long-lived blocks
   // with contiguous ranges) measured slower with it (density 85 -> 73-82 %, profiles/r2s_*)
   p.g.xcd = p.tg.xcd = p.lg.xcd = (c.xcd_map >> (reduces ? 1 : 0)) & 1u;  // bit 0 streaming, 1 reducing
+  // except two-state tiles whose two row bits both sit at chunk bit >= 20 (q2 pairs of far
+  // qubits, row strides >= 16 MiB): XCD order measured better there, reverse_q2 (26,27)
+  // 74.0 -> 75.6 %, while (14,13) drops 73.3 -> 69.1 and (5,20) / (27,0) lose 3-4 points
+  // (profiles/r6/r6o)
+  if (p.tile && two && reduces && p.tg.h == 2 && p.tg.hb0 >= 20) p.tg.xcd = 1;
   p.g.gm = c.gm;
   p.tg.gm = c.gm;
   p.tg.pf = c.tile_pf && p.tg.h == 0;
