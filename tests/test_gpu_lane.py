@@ -165,3 +165,86 @@ def test_diag_reverse_every_pair(prec, n, monkeypatch):
     monkeypatch.setenv("QDC_FUSE", "0")
     bad = _reverse_failures(prec, n, diag_only=True)
     assert not bad, "; ".join(bad)
+
+
+def _large_circuit(n, seed=5):
+    """The gate list of _large_reverse and its seeded matrices."""
+    rng = np.random.default_rng(seed)
+    ins = [(O.VAR_Q1, (p,)) for p in (0, 1, 3, 5, n - 5)]
+    ins += [(O.VAR_Q2, pr) for pr in ((0, 1), (1, 2), (3, 5), (5, 2), (n - 1, 4))]
+    ins += [(O.VAR_Q2_DIAG, pr) for pr in ((0, 1), (n - 5, n - 1), (2, 9))]
+    ins += [(O.DIFF_Q1_DENSITY, (0,)), (O.DIFF_Q1_DENSITY, (n - 1,))]
+    var = []
+    for k, _ in ins:
+        if k == O.VAR_Q1:
+            var.append(O.haar_unitary(rng, 2))
+        elif k == O.VAR_Q2:
+            var.append(O.haar_unitary(rng, 4))
+        elif k == O.VAR_Q2_DIAG:
+            var.append(np.exp(1j * rng.standard_normal(4)))
+    return ins, var
+
+
+def _large_reverse(prec, n):
+    """A short circuit at a size whose reducing tile launches give each block several tiles
+    (n = 25 f32: 8192 two-state tiles on 4096 blocks): q1 / q2 / diagonal gates at low
+    positions (tiles without row bits: the pipelined path), at far positions (row bits) and a
+    far-far diagonal pair; densities at 0 and n - 1.  Returns the densities, gradients and the
+    uncomputed state (fusion off: the single-gate reverse kernels)."""
+    import quantum_differentiable_circuit as q
+    ins, var = _large_circuit(n)
+    vg = [np.ascontiguousarray(g, dtype=DT[prec]) for g in var]
+    c = q.circuit_class(prec)(n)
+    for kind, pos in ins:
+        c._push(kind, *pos)
+    d = c.forward([], vg)
+    cots = [np.ascontiguousarray(np.diag([1.0, -1.0]), dtype=DT[prec]) for _ in d]
+    g = c.backward(cots, [], vg)
+    return d, g, c.get_state(0)
+
+
+@pytest.mark.parametrize("prec,n", [("f32", 25), ("f64", 24)])
+def test_reverse_pipelined_tiles_large_state(prec, n):
+    """Tile-family blocks with several tiles load the next tile during this tile's math
+    (QDC_TILE_PF, round 6; only reachable at large states): the single-gate reverse sweep with
+    it and without it must agree bit for bit, and both with the oracle's circuit
+    (src/circuit.rs:266-429).  Child processes: the knob is read at context creation."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    from pathlib import Path
+    here = Path(__file__).resolve().parent
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for pf in ("0", "1"):
+            f = os.path.join(td, f"pf{pf}.npz")
+            code = (f"import sys; sys.path[:0] = [{str(here)!r}, {str(here.parent)!r}, "
+                    f"{str(here.parent / 'differentiable-quantum-circuit-cuda_amd')!r}]\n"
+                    "import numpy as np, test_gpu_lane as t\n"
+                    f"d, g, st = t._large_reverse({prec!r}, {n})\n"
+                    f"np.savez({f!r}, d=np.concatenate([np.asarray(x).reshape(-1) for x in d]), "
+                    "g=np.concatenate([np.asarray(x).reshape(-1) for x in g]), st=st)\n")
+            env = dict(os.environ, QDC_FUSE="0", QDC_TILE_PF=pf)
+            r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
+                               text=True, timeout=300)
+            assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+            with np.load(f) as z:
+                out[pf] = {k: z[k] for k in ("d", "g", "st")}
+    for k in ("d", "g", "st"):
+        assert np.array_equal(out["0"][k], out["1"][k]), f"{k} differs with the pipelined tiles"
+    # the oracle on the same circuit (the working-precision matrices, as uploaded)
+    ins, var = _large_circuit(n)
+    o = O.OracleCircuit(n)
+    for kind, pos in ins:
+        o.add(kind, *pos)
+    vg = [np.asarray(g, dtype=DT[prec]).astype(np.complex128) for g in var]
+    od = o.forward([], vg)
+    og = o.backward([np.diag([1.0, -1.0]).astype(np.complex128) for _ in od], [], vg)
+    tol = TOL[prec] * (20 if prec == "f32" else 1)
+    for k, got, want in (("densities", out["1"]["d"], np.concatenate([np.asarray(x).reshape(-1) for x in od])),
+                         ("grads", out["1"]["g"], np.concatenate([np.asarray(x).reshape(-1) for x in og])),
+                         ("uncomputed", out["1"]["st"], o.state)):
+        e = relerr(got, want)
+        print(f"[pf-tiles] {prec} n={n} {k} err={e:.2e}")
+        assert e <= tol, f"{k} err={e:.2e}"
