@@ -157,11 +157,13 @@ def test_lane_every_op_class(prec):
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 @pytest.mark.parametrize("n", [14, 16])
 def test_diag_reverse_every_pair(prec, n, monkeypatch):
-    """The diagonal reverse kernel with k fixed per thread (k_diag_q, qdc_kernels.hpp): at n = 14
-    and 16 the state splits into whole blocks per quadrant, so every ordered pair runs on it —
-    positions at the in-chunk amplitude bit, at thread chunk bits (< 8) and at block chunk bits
-    (one or both: quadrant walks) — uncompute, gradient and pull-back against the oracle's
-    circuit, fusion off (primitives.cu:649-672 via circuit.rs:320-392)."""
+    """The diagonal reverse kernel with k fixed per thread (k_diag_q, qdc_kernels.hpp; 16 chunks
+    in flight per thread, so a block spans 4096 chunks): at n = 16 the state splits into whole
+    blocks per quadrant for every ordered pair, at n = 14 for the pairs with at most one block
+    bit in f32 (both in f64; the others run k_diag) — positions at the in-chunk amplitude bit, at
+    thread chunk bits (< 8) and at block chunk bits (one or both: quadrant walks) — uncompute,
+    gradient and pull-back against the oracle's circuit, fusion off (primitives.cu:649-672 via
+    circuit.rs:320-392)."""
     monkeypatch.setenv("QDC_FUSE", "0")
     bad = _reverse_failures(prec, n, diag_only=True)
     assert not bad, "; ".join(bad)
