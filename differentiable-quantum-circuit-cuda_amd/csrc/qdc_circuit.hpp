@@ -288,6 +288,9 @@ struct Circuit {
   // runs of cotangent injections whose cotangents are all diagonal become one elementwise pass
   // (k_diag_inject; QDC_DIAG_INJECT)
   int diag_inject = 1;
+  // the backward's leading diagonal-injection passes launched before its program is built
+  // (QDC_EARLY_INJECT)
+  int early_inject = 1;
   // read-only passes of one-qubit densities on k_dens1 (register partial sums across a block's
   // tiles, one reduction per block; QDC_DENS1=0: k_fused's per-tile reductions)
   int dens1_kernel = 1;
@@ -428,6 +431,7 @@ struct Circuit {
     if (const char* e = getenv("QDC_RQ_PERM_LOW")) rq_perm_low = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_RQ_GSTAGE")) rq_gstage = atoi(e);
     if (const char* e = getenv("QDC_DIAG_INJECT")) diag_inject = atoi(e);
+    if (const char* e = getenv("QDC_EARLY_INJECT")) early_inject = atoi(e);
     if (const char* e = getenv("QDC_DENS1")) dens1_kernel = atoi(e);
     if (const char* e = getenv("QDC_DENS_SPLIT")) dens_split = atoi(e);
     if (const char* e = getenv("QDC_MIRROR")) mirror = atoi(e);
@@ -2245,6 +2249,23 @@ struct Circuit {
     }
     if (diag_inject) merge_diag_injections(items, pl, dg, gidx);
     ht[2] = hclock::now();
+    // a run of diagonal cotangent injections: one elementwise pass (no pass program)
+    auto run_diag_inject = [&](const Item& item) -> const char* {
+      diag_tab T;
+      const uint32_t ng = diag_table(item, pl, dg, gidx, T);
+      for (auto& s : sh) {
+        QDC_TRY(s.c().use());
+        QDC_TRY(qdc::diag_inject(s.c(), s.state, s.bwd, T, ng, nl, gm, have_bwd));
+      }
+      have_bwd = true;
+      return nullptr;
+    };
+    // the backward's leading diagonal-injection passes need no program: they are launched
+    // before it is built, so the device runs them during the host's build (round 6;
+    // QDC_EARLY_INJECT=0: after)
+    size_t lead = 0;
+    if (!dry && early_inject)
+      for (; lead < items.size() && items[lead].type == 3; ++lead) QDC_TRY(run_diag_inject(items[lead]));
     size_t mats_off = 0;
     const auto tb0 = std::chrono::steady_clock::now();
     QDC_TRY(build_program(items, pl, true, first_inject, cg, vg, gidx, mats_off, var_idx,
@@ -2254,15 +2275,10 @@ struct Circuit {
     if (rq_stats)
       fprintf(stderr, "backward plan+build %.3f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
-    for (const Item& item : items) {
-      if (item.type == 3) {  // a run of diagonal cotangent injections: one elementwise pass
-        diag_tab T;
-        const uint32_t ng = diag_table(item, pl, dg, gidx, T);
-        for (auto& s : sh) {
-          QDC_TRY(s.c().use());
-          QDC_TRY(qdc::diag_inject(s.c(), s.state, s.bwd, T, ng, nl, gm, have_bwd));
-        }
-        have_bwd = true;
+    for (size_t ii = lead; ii < items.size(); ++ii) {
+      const Item& item = items[ii];
+      if (item.type == 3) {
+        QDC_TRY(run_diag_inject(item));
         continue;
       }
       if (item.type == 2) {

@@ -190,6 +190,17 @@ struct Ctx {
   // under every variant and block order tried: a DRAM-mapping effect of the row distance
   // (tools/r5/stream_probe2.hip: plain two-row streams at chunk bit 20 reach 72.6 %)
   uint32_t lane_blk = 1;
+  // Address-map exceptions of the one-state application (f32 n = 28 sweep, every q1 position
+  // and 8 q2 pairs, LANE vs its wave variant vs the tile family, two repeats on one box:
+  // profiles/r6/r6v), keyed by the byte stride 2^b of a target (b = position + 3 in f32, + 4 in
+  // f64).  The tile family streams every far q1 at a flat 73 %; LANE beats it everywhere except
+  // at b = 23 and 27 (q1 20 / 24: 72.0 / 71.5 %), where the pair's two rows collide in the
+  // DRAM map: those run on the tile family (knob QDC_LANE_TILE_BITS, a mask of b).  The wave
+  // variant of LANE beats the block-wide one at b = 15 (q1 12: 80.7 -> 85.0 %) and 23 (q2
+  // (5,20): 72.8 -> 75.0 %) and loses 1-3 points at 9 other placements (knob
+  // QDC_LANE_NOBLK_BITS).
+  uint64_t lane_tile_bits = (1ull << 23) | (1ull << 27);
+  uint64_t lane_noblk_bits = (1ull << 15) | (1ull << 23);
   // reduction arena
   cx* partials = nullptr;  // [FIN_MAX][NBMAX][RED]
   cx* results = nullptr;   // [FIN_MAX][RED] scratch destination for one-shot reductions
@@ -243,6 +254,8 @@ struct Ctx {
     if (const char* e = getenv("QDC_DIAG_RED")) diag_red = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_TILE_PF")) tile_pf = (uint32_t)atoi(e);
     if (const char* e = getenv("QDC_LANE_BLK")) lane_blk = (uint32_t)atoi(e);
+    if (const char* e = getenv("QDC_LANE_TILE_BITS")) lane_tile_bits = strtoull(e, nullptr, 0);
+    if (const char* e = getenv("QDC_LANE_NOBLK_BITS")) lane_noblk_bits = strtoull(e, nullptr, 0);
     if (const char* e = getenv("QDC_LANE_U")) {
       unsigned u0 = 0, u1 = 0, u2 = 0;
       if (sscanf(e, "%u,%u,%u", &u0, &u1, &u2) == 3) {
@@ -812,12 +825,17 @@ inline Plan plan_for(const Ctx& c, uint32_t n, uint32_t pos2, uint32_t pos1, boo
   Plan p;
   const uint32_t lcls = writes_both ? 0u : reduces ? 2u : 1u;  // QDC_LANE bit
   const uint32_t rcap = writes_both ? c.rev_red_cap : c.red_cap;
-  if (!((c.lane_ops >> lcls) & 1u) ||
+  // byte-stride bits of the targets (Ctx::lane_tile_bits / lane_noblk_bits)
+  constexpr uint32_t CXB = sizeof(cx) == 8 ? 3u : 4u;
+  const uint64_t tb = ((uint64_t)1 << (pos1 + CXB)) | ((uint64_t)1 << (pos2 + CXB));
+  const bool apply1 = lcls == 1 && !two;  // a one-state application (not an injection)
+  const bool lane_tile = apply1 && R == 2 && (tb & c.lane_tile_bits) != 0;
+  if (!((c.lane_ops >> lcls) & 1u) || lane_tile ||
       !plan_lane(n, R, pos2, pos1, rcap, reduces, p, c.lane_u[lcls])) {
     p = plan_gate(n, R, pos2, pos1, two, reduces ? rcap : c.grid_cap,
                   (c.tile_far >> cls) & 1u, c.tile2_wide, c.tile1_wide);
     if (!p.tile && p.g.it < c.direct_it) p.g.it = c.direct_it;
-  } else if (lcls == 1 && c.lane_blk && p.lg.nf > 0) {
+  } else if (lcls == 1 && c.lane_blk && p.lg.nf > 0 && !(apply1 && (tb & c.lane_noblk_bits))) {
     // a far target: the block-wide variant, when the state holds a 1024-chunk unit
     Plan q;
     if (plan_lane(n, R, pos2, pos1, c.red_cap, reduces, q, 1, 10)) p = q;
